@@ -1,0 +1,267 @@
+// mpcqp_capi.cpp — extern "C" boundary (include/mpcqp.h) over the HIP kernels.
+//
+// Replaces, per batch of robots, the OsqpEigen::Solver lifecycle of the reference
+// (A1RobotControl.h:67, A1RobotControl.cpp:522-555) and ConvexMpc's construction
+// (ConvexMpc.cpp:7-68).  No exception crosses this boundary.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+
+#include "../../include/mpcqp.h"
+#include "../../include/mpcqp_debug.h"
+#include "mpcqp_internal.h"
+
+struct mpcqp_handle {
+  mpcqp_params p;
+  int device = 0;
+  int slots = 0;             // resident workgroups per device (occupancy x CUs), informational
+  double* work = nullptr;    // per-instance 128x128 binary64 workspace (scaled Hessian)
+  size_t work_cap = 0;       // instances the workspace can hold
+  // host wrapper staging
+  double* d_recs = nullptr;
+  mpcqp_result* d_res = nullptr;
+  double* d_sol = nullptr;
+  size_t cap = 0;
+  char err[256] = {0};
+};
+
+namespace {
+
+int set_hip_error(mpcqp_handle* h, hipError_t e, const char* where) {
+  if (h) snprintf(h->err, sizeof(h->err), "%s: %s", where, hipGetErrorString(e));
+  return MPCQP_ERR_HIP;
+}
+
+bool params_valid(const mpcqp_params* p) {
+  if (!p) return false;
+  if (p->horizon < 1 || p->horizon > MPCQP_MAX_HORIZON) return false;
+  if (p->max_iter < 1 || p->scaling < 0 || p->check_termination < 0) return false;
+  if (p->adaptive_rho && p->adaptive_rho_interval <= 0) return false;  // wall-clock interval unsupported
+  if (!(p->rho > 0) || !(p->sigma > 0) || !(p->alpha > 0 && p->alpha < 2)) return false;
+  if (!(p->eps_abs >= 0) || !(p->eps_rel >= 0)) return false;
+  if (p->scaled_termination != 0) return false;  // reference uses the default (0)
+  for (int i = 0; i < MPCQP_STATE_DIM; ++i)
+    if (!isfinite(p->q_weights[i])) return false;
+  for (int i = 0; i < MPCQP_NUM_DOF; ++i)
+    if (!isfinite(p->r_weights[i])) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+void mpcqp_default_params(mpcqp_params* p, int32_t horizon) {
+  if (!p) return;
+  memset(p, 0, sizeof(*p));
+  p->horizon = horizon;
+  p->max_iter = 4000;
+  p->scaling = 10;
+  p->check_termination = 25;
+  p->adaptive_rho = 1;
+  p->adaptive_rho_interval = 25;
+  p->scaled_termination = 0;
+  p->warm_start = 0;
+  // Go1CtrlStates.hpp:203-249 defaults
+  const double q[13] = {80.0, 80.0, 1.0, 0.0, 0.0, 270.0, 1.0, 1.0, 20.0, 20.0, 20.0, 20.0, 0.0};
+  const double r[12] = {1e-5, 1e-5, 1e-6, 1e-5, 1e-5, 1e-6, 1e-5, 1e-5, 1e-6, 1e-5, 1e-5, 1e-6};
+  memcpy(p->q_weights, q, sizeof(q));
+  memcpy(p->r_weights, r, sizeof(r));
+  p->rho = 0.1;
+  p->sigma = 1e-6;
+  p->alpha = 1.6;
+  p->eps_abs = 1e-3;
+  p->eps_rel = 1e-3;
+  p->eps_prim_inf = 1e-4;
+  p->eps_dual_inf = 1e-4;
+  p->adaptive_rho_tolerance = 5.0;
+}
+
+int32_t mpcqp_record_size(int32_t horizon) {
+  if (horizon < 1) return 0;
+  return MPCQP_REC_SIZE(horizon);
+}
+
+int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** out) {
+  if (!out) return MPCQP_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (!params_valid(params)) return MPCQP_ERR_INVALID_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MPCQP_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return MPCQP_ERR_INVALID_ARG;
+  mpcqp_handle* h = new (std::nothrow) mpcqp_handle();
+  if (!h) return MPCQP_ERR_ALLOC;
+  h->p = *params;
+  h->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) { delete h; return MPCQP_ERR_HIP; }
+  int cus = 0, per_cu = 0;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e == hipSuccess) e = mpcqp::occupancy_any(params->horizon, &per_cu);
+  if (e != hipSuccess || cus <= 0) { delete h; return MPCQP_ERR_HIP; }
+  if (per_cu < 1) per_cu = 1;
+  h->slots = cus * per_cu;
+  *out = h;
+  return MPCQP_OK;
+}
+
+int32_t mpcqp_destroy(mpcqp_handle* h) {
+  if (!h) return MPCQP_ERR_INVALID_ARG;
+  (void)hipSetDevice(h->device);
+  (void)hipFree(h->work);
+  (void)hipFree(h->d_recs);
+  (void)hipFree(h->d_res);
+  (void)hipFree(h->d_sol);
+  delete h;
+  return MPCQP_OK;
+}
+
+static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32_t batch,
+                                 mpcqp_result* d_results, double* d_solution, double* d_trace,
+                                 int32_t trace_cap, void* stream) {
+  if (!h || batch < 0 || (batch > 0 && (!d_records || !d_results))) return MPCQP_ERR_INVALID_ARG;
+  if (batch == 0) return MPCQP_OK;
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
+  if ((size_t)batch > h->work_cap) {
+    // grow-only; a capture-safe caller pre-sizes with mpcqp_reserve()
+    e = hipStreamSynchronize((hipStream_t)stream);
+    if (e == hipSuccess) e = hipFree(h->work);
+    h->work = nullptr;
+    h->work_cap = 0;
+    if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * (size_t)mpcqp::NP * mpcqp::NP * batch);
+    if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
+    h->work_cap = batch;
+  }
+  mpcqp::LaunchArgs a;
+  a.recs = d_records;
+  a.batch = batch;
+  a.results = d_results;
+  a.solution = d_solution;
+  a.work = h->work;
+  a.trace = d_trace;
+  a.trace_cap = d_trace ? trace_cap : 0;
+  a.grid = batch;
+  a.stream = stream;
+  a.p = h->p;
+  e = mpcqp::launch_solve_any(a);
+  if (e != hipSuccess) return set_hip_error(h, e, "solve_kernel launch");
+  return MPCQP_OK;
+}
+
+int32_t mpcqp_solve_batch_device(mpcqp_handle* h, const double* d_records, int32_t batch,
+                                 mpcqp_result* d_results, double* d_solution, void* stream) {
+  return solve_device_impl(h, d_records, batch, d_results, d_solution, nullptr, 0, stream);
+}
+
+int32_t mpcqp_debug_solve_trace_device(mpcqp_handle* h, const double* d_records, int32_t batch,
+                                       mpcqp_result* d_results, double* d_solution,
+                                       double* d_trace, int32_t trace_cap, void* stream) {
+  return solve_device_impl(h, d_records, batch, d_results, d_solution, d_trace, trace_cap, stream);
+}
+
+int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t batch,
+                               mpcqp_result* h_results, double* h_solution) {
+  if (!h || batch < 0 || (batch > 0 && (!h_records || !h_results))) return MPCQP_ERR_INVALID_ARG;
+  if (batch == 0) return MPCQP_OK;
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
+  const size_t rs = (size_t)MPCQP_REC_SIZE(h->p.horizon);
+  const size_t n = (size_t)MPCQP_NUM_DOF * h->p.horizon;
+  if ((size_t)batch > h->cap) {
+    (void)hipFree(h->d_recs);
+    (void)hipFree(h->d_res);
+    (void)hipFree(h->d_sol);
+    h->d_recs = nullptr; h->d_res = nullptr; h->d_sol = nullptr; h->cap = 0;
+    e = hipMalloc(&h->d_recs, sizeof(double) * rs * batch);
+    if (e == hipSuccess) e = hipMalloc(&h->d_res, sizeof(mpcqp_result) * batch);
+    if (e == hipSuccess) e = hipMalloc(&h->d_sol, sizeof(double) * n * batch);
+    if (e != hipSuccess) return set_hip_error(h, e, "hipMalloc");
+    h->cap = batch;
+  }
+  e = hipMemcpy(h->d_recs, h_records, sizeof(double) * rs * batch, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipMemcpy H2D");
+  int32_t rc = solve_device_impl(h, h->d_recs, batch, h->d_res, h_solution ? h->d_sol : nullptr,
+                                 nullptr, 0, nullptr);
+  if (rc != MPCQP_OK) return rc;
+  e = hipMemcpy(h_results, h->d_res, sizeof(mpcqp_result) * batch, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && h_solution)
+    e = hipMemcpy(h_solution, h->d_sol, sizeof(double) * n * batch, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipMemcpy D2H");
+  return MPCQP_OK;
+}
+
+int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t batch, double* d_P,
+                              double* d_q, double* d_l, double* d_u, void* stream) {
+  if (!h || batch < 0 || (batch > 0 && (!d_records || !d_P || !d_q || !d_l || !d_u)))
+    return MPCQP_ERR_INVALID_ARG;
+  if (batch == 0) return MPCQP_OK;
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
+  mpcqp::LaunchArgs a;
+  memset(&a, 0, sizeof(a));
+  a.recs = d_records;
+  a.batch = batch;
+  a.stream = stream;
+  a.p = h->p;
+  e = mpcqp::launch_build_any(a, d_P, d_q, d_l, d_u);
+  if (e != hipSuccess) return set_hip_error(h, e, "build_qp_kernel launch");
+  return MPCQP_OK;
+}
+
+const char* mpcqp_status_str(int32_t s) {
+  switch (s) {
+    case MPCQP_STATUS_SOLVED: return "solved";
+    case MPCQP_STATUS_SOLVED_INACCURATE: return "solved inaccurate";
+    case MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE: return "primal infeasible inaccurate";
+    case MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE: return "dual infeasible inaccurate";
+    case MPCQP_STATUS_MAX_ITER_REACHED: return "maximum iterations reached";
+    case MPCQP_STATUS_PRIMAL_INFEASIBLE: return "primal infeasible";
+    case MPCQP_STATUS_DUAL_INFEASIBLE: return "dual infeasible";
+    case MPCQP_STATUS_NON_CVX: return "problem non convex";
+    case MPCQP_STATUS_NAN_INPUT: return "non-finite input";
+    case MPCQP_STATUS_UNSOLVED: return "unsolved";
+    default: return "unknown status";
+  }
+}
+
+const char* mpcqp_error_str(int32_t err) {
+  switch (err) {
+    case MPCQP_OK: return "ok";
+    case MPCQP_ERR_INVALID_ARG: return "invalid argument";
+    case MPCQP_ERR_HIP: return "HIP runtime error";
+    case MPCQP_ERR_NO_DEVICE: return "no HIP device";
+    case MPCQP_ERR_ALLOC: return "device allocation failed";
+    default: return "unknown error";
+  }
+}
+
+const char* mpcqp_last_error(mpcqp_handle* h) { return h ? h->err : "null handle"; }
+
+int32_t mpcqp_abi_sizes(int32_t* params_size, int32_t* result_size) {
+  if (params_size) *params_size = (int32_t)sizeof(mpcqp_params);
+  if (result_size) *result_size = (int32_t)sizeof(mpcqp_result);
+  return MPCQP_OK;
+}
+
+int32_t mpcqp_handle_slots(mpcqp_handle* h) { return h ? h->slots : 0; }
+
+int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {
+  if (!h || batch < 0) return MPCQP_ERR_INVALID_ARG;
+  if ((size_t)batch <= h->work_cap) return MPCQP_OK;
+  hipError_t e = hipSetDevice(h->device);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipFree(h->work);
+  h->work = nullptr;
+  h->work_cap = 0;
+  if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * (size_t)mpcqp::NP * mpcqp::NP * batch);
+  if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
+  h->work_cap = batch;
+  return MPCQP_OK;
+}
+int32_t mpcqp_solve_threads(void) { return mpcqp::solve_threads(); }
+
+}  // extern "C"

@@ -1,0 +1,166 @@
+"""ctypes view of libmpcqp.so (include/mpcqp.h, include/mpcqp_debug.h).
+
+The shared library is built in-tree (go1-qp-mpc-controller_amd/lib/libmpcqp.so) by
+``make -C go1-qp-mpc-controller_amd`` / ``__graft_entry__.build()``.  There is no fallback:
+if the library is missing or has no HIP device, the call fails loudly.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libmpcqp.so")
+
+STATE_DIM, NUM_LEG, NUM_DOF, CONSTRAINT_DIM = 13, 4, 12, 20
+MAX_HORIZON = 10
+OSQP_INFTY = 1e30
+
+# record layout (include/mpcqp.h MPCQP_REC_*)
+REC_X0, REC_EULER, REC_ROT, REC_INERTIA = 0, 13, 16, 25
+REC_MASS, REC_MU, REC_FZMIN, REC_FZMAX, REC_DT, REC_CONTACTS, REC_XREF = 34, 35, 36, 37, 38, 39, 44
+
+
+def rec_feet(N):
+    return REC_XREF + 13 * N
+
+
+def rec_size(N):
+    return REC_XREF + 25 * N + (N & 1)
+
+
+# OSQP 0.6 status values
+STATUS_SOLVED = 1
+STATUS_SOLVED_INACCURATE = 2
+STATUS_PRIMAL_INFEASIBLE_INACCURATE = 3
+STATUS_DUAL_INFEASIBLE_INACCURATE = 4
+STATUS_MAX_ITER_REACHED = -2
+STATUS_PRIMAL_INFEASIBLE = -3
+STATUS_DUAL_INFEASIBLE = -4
+STATUS_NON_CVX = -7
+STATUS_NAN_INPUT = -100
+STATUS_UNSOLVED = -10
+
+ERR_OK, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_ALLOC = 0, 1, 2, 3, 4
+
+
+class Params(ctypes.Structure):
+    """mpcqp_params."""
+    _fields_ = [
+        ("horizon", ctypes.c_int32), ("max_iter", ctypes.c_int32), ("scaling", ctypes.c_int32),
+        ("check_termination", ctypes.c_int32), ("adaptive_rho", ctypes.c_int32),
+        ("adaptive_rho_interval", ctypes.c_int32), ("scaled_termination", ctypes.c_int32),
+        ("warm_start", ctypes.c_int32),
+        ("q_weights", ctypes.c_double * 13), ("r_weights", ctypes.c_double * 12),
+        ("rho", ctypes.c_double), ("sigma", ctypes.c_double), ("alpha", ctypes.c_double),
+        ("eps_abs", ctypes.c_double), ("eps_rel", ctypes.c_double),
+        ("eps_prim_inf", ctypes.c_double), ("eps_dual_inf", ctypes.c_double),
+        ("adaptive_rho_tolerance", ctypes.c_double),
+    ]
+
+
+class Result(ctypes.Structure):
+    """mpcqp_result."""
+    _fields_ = [
+        ("u0", ctypes.c_double * 12), ("f_body", ctypes.c_double * 12),
+        ("obj_val", ctypes.c_double), ("pri_res", ctypes.c_double), ("dua_res", ctypes.c_double),
+        ("rho", ctypes.c_double), ("status", ctypes.c_int32), ("iters", ctypes.c_int32),
+        ("rho_updates", ctypes.c_int32), ("nan_legs", ctypes.c_int32),
+    ]
+
+
+RESULT_DTYPE = np.dtype([
+    ("u0", "f8", 12), ("f_body", "f8", 12), ("obj_val", "f8"), ("pri_res", "f8"),
+    ("dua_res", "f8"), ("rho", "f8"), ("status", "i4"), ("iters", "i4"),
+    ("rho_updates", "i4"), ("nan_legs", "i4"),
+])
+RESULT_DOUBLES = RESULT_DTYPE.itemsize // 8  # 30
+
+# every symbol declared by include/mpcqp.h and include/mpcqp_debug.h
+EXPORTED = [
+    "mpcqp_default_params", "mpcqp_record_size", "mpcqp_create", "mpcqp_destroy", "mpcqp_reserve",
+    "mpcqp_solve_batch_device", "mpcqp_solve_batch_host", "mpcqp_build_qp_device",
+    "mpcqp_status_str", "mpcqp_error_str", "mpcqp_last_error",
+    "mpcqp_debug_solve_trace_device", "mpcqp_abi_sizes", "mpcqp_handle_slots", "mpcqp_solve_threads",
+]
+
+_lib = None
+
+
+class MpcQpError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libmpcqp.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MpcQpError(f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, dp, i32 = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int32
+    L.mpcqp_default_params.argtypes = [ctypes.POINTER(Params), i32]
+    L.mpcqp_default_params.restype = None
+    L.mpcqp_record_size.argtypes = [i32]
+    L.mpcqp_record_size.restype = i32
+    L.mpcqp_create.argtypes = [ctypes.POINTER(Params), i32, ctypes.POINTER(vp)]
+    L.mpcqp_create.restype = i32
+    L.mpcqp_destroy.argtypes = [vp]
+    L.mpcqp_destroy.restype = i32
+    L.mpcqp_reserve.argtypes = [vp, i32]
+    L.mpcqp_reserve.restype = i32
+    L.mpcqp_solve_batch_device.argtypes = [vp, vp, i32, vp, vp, vp]
+    L.mpcqp_solve_batch_device.restype = i32
+    L.mpcqp_solve_batch_host.argtypes = [vp, dp, i32, vp, dp]
+    L.mpcqp_solve_batch_host.restype = i32
+    L.mpcqp_build_qp_device.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+    L.mpcqp_build_qp_device.restype = i32
+    L.mpcqp_status_str.argtypes = [i32]
+    L.mpcqp_status_str.restype = ctypes.c_char_p
+    L.mpcqp_error_str.argtypes = [i32]
+    L.mpcqp_error_str.restype = ctypes.c_char_p
+    L.mpcqp_last_error.argtypes = [vp]
+    L.mpcqp_last_error.restype = ctypes.c_char_p
+    L.mpcqp_debug_solve_trace_device.argtypes = [vp, vp, i32, vp, vp, vp, i32, vp]
+    L.mpcqp_debug_solve_trace_device.restype = i32
+    L.mpcqp_abi_sizes.argtypes = [ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    L.mpcqp_abi_sizes.restype = i32
+    L.mpcqp_handle_slots.argtypes = [vp]
+    L.mpcqp_handle_slots.restype = i32
+    L.mpcqp_solve_threads.argtypes = []
+    L.mpcqp_solve_threads.restype = i32
+    ps, rs = i32(0), i32(0)
+    L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
+    if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):
+        raise MpcQpError(f"ABI mismatch: C sizes {ps.value}/{rs.value} vs ctypes "
+                         f"{ctypes.sizeof(Params)}/{ctypes.sizeof(Result)}")
+    _lib = L
+    return L
+
+
+def default_params(horizon=10, **over):
+    """mpcqp_default_params + keyword overrides (q_weights/r_weights accept sequences)."""
+    p = Params()
+    load().mpcqp_default_params(ctypes.byref(p), horizon)
+    for k, v in over.items():
+        if k in ("q_weights", "r_weights"):
+            arr = getattr(p, k)
+            for i, x in enumerate(v):
+                arr[i] = float(x)
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def check(rc, handle=None, what="mpcqp"):
+    if rc != ERR_OK:
+        L = load()
+        msg = L.mpcqp_error_str(rc).decode()
+        if handle:
+            msg += ": " + L.mpcqp_last_error(handle).decode()
+        raise MpcQpError(f"{what} failed ({rc}): {msg}")
+
+
+def status_str(s):
+    return load().mpcqp_status_str(int(s)).decode()

@@ -1,0 +1,83 @@
+"""Handle-level Python API over libmpcqp (mirrors the C ABI one to one).
+
+``MpcQpSolver`` plays the role of the reference's long-lived ``OsqpEigen::Solver`` member
+(A1RobotControl.h:67) for a whole batch of robots.  Device buffers are passed as raw pointers
+(e.g. ``torch.Tensor.data_ptr()``) and streams as integer hipStream_t handles
+(``torch.cuda.current_stream().cuda_stream``); torch is plumbing only and never imported here.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import RESULT_DTYPE, Params, check, load, rec_size
+
+
+class MpcQpSolver:
+    def __init__(self, params: Params = None, horizon=10, device=0):
+        L = load()
+        self.params = params if params is not None else _lib.default_params(horizon)
+        self.horizon = self.params.horizon
+        self.n = 12 * self.horizon
+        self.m = 20 * self.horizon
+        self.rec_size = rec_size(self.horizon)
+        h = ctypes.c_void_p()
+        check(L.mpcqp_create(ctypes.byref(self.params), int(device), ctypes.byref(h)), None, "mpcqp_create")
+        self._h = h
+        self._L = L
+
+    # -- lifecycle -------------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.mpcqp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def slots(self):
+        return self._L.mpcqp_handle_slots(self._h)
+
+    def reserve(self, batch):
+        check(self._L.mpcqp_reserve(self._h, int(batch)), self._h, "mpcqp_reserve")
+
+    # -- device-pointer API ------------------------------------------------------------------------
+    def solve_device(self, d_records, batch, d_results, d_solution=0, stream=0):
+        """mpcqp_solve_batch_device: records/results/solution are device pointers (ints)."""
+        check(self._L.mpcqp_solve_batch_device(self._h, d_records, int(batch), d_results,
+                                               d_solution or None, stream or None),
+              self._h, "mpcqp_solve_batch_device")
+
+    def solve_device_trace(self, d_records, batch, d_results, d_solution, d_trace, trace_cap, stream=0):
+        check(self._L.mpcqp_debug_solve_trace_device(self._h, d_records, int(batch), d_results,
+                                                     d_solution or None, d_trace, int(trace_cap),
+                                                     stream or None),
+              self._h, "mpcqp_debug_solve_trace_device")
+
+    def build_qp_device(self, d_records, batch, d_P, d_q, d_l, d_u, stream=0):
+        check(self._L.mpcqp_build_qp_device(self._h, d_records, int(batch), d_P, d_q, d_l, d_u,
+                                            stream or None),
+              self._h, "mpcqp_build_qp_device")
+
+    # -- host convenience --------------------------------------------------------------------------
+    def solve_host(self, records, want_solution=False):
+        """mpcqp_solve_batch_host on numpy records [B, rec_size]; returns structured results."""
+        recs = np.ascontiguousarray(records, dtype=np.float64).reshape(-1, self.rec_size)
+        B = recs.shape[0]
+        res = np.zeros(B, dtype=RESULT_DTYPE)
+        sol = np.zeros((B, self.n)) if want_solution else None
+        dp = ctypes.POINTER(ctypes.c_double)
+        check(self._L.mpcqp_solve_batch_host(
+            self._h, recs.ctypes.data_as(dp), B, res.ctypes.data,
+            sol.ctypes.data_as(dp) if sol is not None else None), self._h, "mpcqp_solve_batch_host")
+        return (res, sol) if want_solution else res

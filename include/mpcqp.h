@@ -1,0 +1,164 @@
+/*
+ * mpcqp.h — C ABI of the MI355X-native batched convex-MPC QP engine.
+ *
+ * Drop-in boundary for the per-control-cycle ground-reaction-force (GRF) solve of
+ * zerenluo123/Go1-QP-MPC-Controller.  The reference performs, per robot and per tick:
+ *
+ *   ConvexMpc ctor/reset                      src/a1_cpp/src/ConvexMpc.cpp:7-108
+ *   calculate_A_mat_c / calculate_B_mat_c     src/a1_cpp/src/ConvexMpc.cpp:110-143
+ *   state_space_discretization                src/a1_cpp/src/ConvexMpc.cpp:145-156
+ *   calculate_qp_mats (A_qp, B_qp, H, g, l/u) src/a1_cpp/src/ConvexMpc.cpp:158-245
+ *   OsqpEigen setup + solve (OSQP 0.6.x)      src/a1_cpp/src/A1RobotControl.cpp:522-555
+ *   extraction f_i = R^T u[3i:3i+3]           src/a1_cpp/src/A1RobotControl.cpp:555-561
+ *
+ * Every entry point below replaces one of those interfaces for a whole *batch* of robots.
+ * The header is plain C: no HIP, Eigen or torch types.  Streams are passed as opaque
+ * `void*` (a hipStream_t; NULL = the default stream).
+ *
+ * Arithmetic is IEEE binary64 (the reference computes in double everywhere).
+ *
+ * Threading: a handle is bound to one device and is not thread-safe; use one handle per
+ * host thread / stream.  Inputs are read once per call (snapshot semantics).
+ * Errors never throw across this boundary: every function returns an mpcqp_error code.
+ */
+#ifndef MPCQP_H_
+#define MPCQP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- dimensions (reference: src/a1_cpp/src/A1Params.h:26-34) ------------------------ */
+#define MPCQP_STATE_DIM 13      /* MPC_STATE_DIM: [rpy, p, w, v, g]                       */
+#define MPCQP_NUM_LEG 4         /* NUM_LEG (FL, FR, RL, RR)                               */
+#define MPCQP_NUM_DOF 12        /* NUM_DOF: 3 GRF components x 4 legs per horizon step     */
+#define MPCQP_CONSTRAINT_DIM 20 /* MPC_CONSTRAINT_DIM: 5 friction-pyramid rows x 4 legs    */
+#define MPCQP_MAX_HORIZON 10    /* horizons 1..10 are served by the register-resident path */
+#define MPCQP_OSQP_INFTY 1e30   /* OsqpEigen::INFTY == OSQP_INFTY (OSQP 0.6 constants.h)  */
+
+/* ---- per-instance problem record (all binary64, contiguous) ----------------------------
+ * One record describes exactly the inputs ConvexMpc::calculate_qp_mats and the MPC branch
+ * of A1RobotControl::compute_grf consume.  Offsets are in doubles.                        */
+#define MPCQP_REC_X0 0        /* [13] mpc_states x0 (A1RobotControl.cpp:452-456)                 */
+#define MPCQP_REC_EULER 13    /* [3]  euler given to calculate_A_mat_c (only yaw is used, :116)  */
+#define MPCQP_REC_ROT 16      /* [9]  root_rot_mat, row-major (calculate_B_mat_c arg)            */
+#define MPCQP_REC_INERTIA 25  /* [9]  trunk inertia, body frame, row-major                       */
+#define MPCQP_REC_MASS 34     /* robot_mass                                                       */
+#define MPCQP_REC_MU 35       /* friction coefficient (ConvexMpc.cpp:8 hard-codes 0.3)            */
+#define MPCQP_REC_FZMIN 36    /* fz_min (ConvexMpc.cpp:223: 0)                                    */
+#define MPCQP_REC_FZMAX 37    /* fz_max (ConvexMpc.cpp:224: 180)                                  */
+#define MPCQP_REC_DT 38       /* mpc_dt used by state_space_discretization (A1RobotControl:462)  */
+#define MPCQP_REC_CONTACTS 39 /* [4]  contacts[i] as 0.0 / 1.0 (bounds, ConvexMpc.cpp:225-241)    */
+#define MPCQP_REC_XREF 44     /* [13N] mpc_states_d                                               */
+/* feet: [N][4][3] foot_pos used for B_c at horizon step i (foot_pos_abs in compute_grf, the
+ * per-step shifted foot_pos_abs_mpc in test_mpc.cpp:105-115), at MPCQP_REC_XREF + 13N           */
+#define MPCQP_REC_FEET(N) (MPCQP_REC_XREF + 13 * (N))
+#define MPCQP_REC_SIZE(N) (MPCQP_REC_XREF + 25 * (N) + ((N)&1))
+
+/* ---- solver settings: OSQP 0.6 defaults + the reference's overrides -------------------
+ * (A1RobotControl.cpp:522-538 sets only verbosity=false and warm_start; everything else
+ * is osqp_set_default_settings).  adaptive_rho_interval: OSQP's 0 means "derive from
+ * wall-clock" (non-reproducible); the engine requires a fixed interval (default 25).      */
+typedef struct mpcqp_params {
+  int32_t horizon;                /* N, 1..MPCQP_MAX_HORIZON (PLAN_HORIZON = 10)            */
+  int32_t max_iter;               /* 4000                                                   */
+  int32_t scaling;                /* 10 Ruiz passes                                          */
+  int32_t check_termination;      /* 25                                                      */
+  int32_t adaptive_rho;           /* 1                                                       */
+  int32_t adaptive_rho_interval;  /* 25 (fixed; see above)                                   */
+  int32_t scaled_termination;     /* 0                                                       */
+  int32_t warm_start;             /* 0: cold start every solve (test_mpc.cpp:133)            */
+  double q_weights[MPCQP_STATE_DIM]; /* ConvexMpc ctor arg; Q = diag(2 q) tiled (:16-23)    */
+  double r_weights[MPCQP_NUM_DOF];   /* ConvexMpc ctor arg; R = diag(2 r) tiled (:37-44)    */
+  double rho;                     /* 0.1                                                     */
+  double sigma;                   /* 1e-6                                                    */
+  double alpha;                   /* 1.6                                                     */
+  double eps_abs, eps_rel;        /* 1e-3, 1e-3                                              */
+  double eps_prim_inf, eps_dual_inf; /* 1e-4, 1e-4                                           */
+  double adaptive_rho_tolerance;  /* 5                                                       */
+} mpcqp_params;
+
+/* ---- per-instance result --------------------------------------------------------------- */
+typedef struct mpcqp_result {
+  double u0[MPCQP_NUM_DOF];     /* solution.segment(0,12): world-frame GRF of horizon step 0 */
+  double f_body[MPCQP_NUM_DOF]; /* compute_grf output: R^T u0[3i:3i+3] per leg (leg-major);
+                                   legs whose norm is NaN are left 0 and flagged in nan_legs  */
+  double obj_val;               /* unscaled objective 1/2 x'Px + q'x (OSQP info->obj_val)     */
+  double pri_res, dua_res;      /* unscaled residuals at the last termination check          */
+  double rho;                   /* final rho                                                  */
+  int32_t status;               /* MPCQP_STATUS_* (numerically equal to OSQP 0.6 status_val)  */
+  int32_t iters;                /* OSQP info->iter                                            */
+  int32_t rho_updates;          /* OSQP info->rho_updates                                     */
+  int32_t nan_legs;             /* bit i set: leg i solution had a NaN norm                   */
+} mpcqp_result;
+
+/* OSQP 0.6 status values (constants.h) */
+enum {
+  MPCQP_STATUS_SOLVED = 1,
+  MPCQP_STATUS_SOLVED_INACCURATE = 2,
+  MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE = 3,
+  MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE = 4,
+  MPCQP_STATUS_MAX_ITER_REACHED = -2,
+  MPCQP_STATUS_PRIMAL_INFEASIBLE = -3,
+  MPCQP_STATUS_DUAL_INFEASIBLE = -4,
+  MPCQP_STATUS_NON_CVX = -7,
+  MPCQP_STATUS_NAN_INPUT = -100, /* engine-specific: a NaN/inf in the instance's record      */
+  MPCQP_STATUS_UNSOLVED = -10
+};
+
+/* call-level error codes */
+enum {
+  MPCQP_OK = 0,
+  MPCQP_ERR_INVALID_ARG = 1,
+  MPCQP_ERR_HIP = 2,
+  MPCQP_ERR_NO_DEVICE = 3,
+  MPCQP_ERR_ALLOC = 4
+};
+
+typedef struct mpcqp_handle mpcqp_handle;
+
+/* Fill *p with the reference's settings for horizon N (OSQP 0.6 defaults, Go1 weights from
+ * src/go1_rl_ctrl_cpp/src/Go1CtrlStates.hpp:203-249, fixed adaptive-rho interval 25). */
+void mpcqp_default_params(mpcqp_params* p, int32_t horizon);
+
+/* Number of doubles in one problem record for horizon N. */
+int32_t mpcqp_record_size(int32_t horizon);
+
+/* Replaces the ConvexMpc ctor + OsqpEigen::Solver construction (ConvexMpc.cpp:7-68,
+ * A1RobotControl.h:67): uploads weights/settings to `device`. */
+int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** out);
+int32_t mpcqp_destroy(mpcqp_handle* h);
+
+/* Pre-size the per-instance device workspace (128x128 binary64 per robot) so that later
+ * mpcqp_solve_batch_device calls with batch <= `batch` never allocate (hipGraph-capture safe). */
+int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch);
+
+/* Replaces calculate_A/B_mat_c + discretization + calculate_qp_mats + OSQP initSolver/solve
+ * + extraction (A1RobotControl.cpp:446-561) for `batch` robots.  All pointers are DEVICE
+ * pointers; asynchronous on `stream`.
+ *   d_records  [batch][mpcqp_record_size(N)]
+ *   d_results  [batch] mpcqp_result
+ *   d_solution [batch][12N] full unscaled primal solution, or NULL                       */
+int32_t mpcqp_solve_batch_device(mpcqp_handle* h, const double* d_records, int32_t batch,
+                                 mpcqp_result* d_results, double* d_solution, void* stream);
+
+/* Host-pointer convenience wrapper (copies in, solves, copies out, synchronizes). */
+int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t batch,
+                               mpcqp_result* h_results, double* h_solution);
+
+/* Formulation only (ConvexMpc::calculate_qp_mats): dense Hessian (full symmetric, row-major
+ * [12N][12N]), gradient [12N], bounds l/u [20N] per instance.  DEVICE pointers. */
+int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t batch,
+                              double* d_P, double* d_q, double* d_l, double* d_u, void* stream);
+
+const char* mpcqp_status_str(int32_t status);
+const char* mpcqp_error_str(int32_t err);
+/* Last HIP error string recorded by the handle (for MPCQP_ERR_HIP). */
+const char* mpcqp_last_error(mpcqp_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCQP_H_ */

@@ -1,0 +1,34 @@
+/*
+ * mpcqp_debug.h — diagnostic entry points of libmpcqp (not needed by a drop-in caller).
+ */
+#ifndef MPCQP_DEBUG_H_
+#define MPCQP_DEBUG_H_
+
+#include <stdint.h>
+
+#include "mpcqp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same as mpcqp_solve_batch_device, and additionally records, for the first `trace_cap`
+ * instances, up to 64 termination checks each as {iter, pri_res, dua_res, rho} into
+ * d_trace[trace_cap][64][4] (device pointer; pre-fill with NaN to see the count). */
+int32_t mpcqp_debug_solve_trace_device(mpcqp_handle* h, const double* d_records, int32_t batch,
+                                       mpcqp_result* d_results, double* d_solution,
+                                       double* d_trace, int32_t trace_cap, void* stream);
+
+/* sizeof(mpcqp_params), sizeof(mpcqp_result) as compiled (ABI check for bindings). */
+int32_t mpcqp_abi_sizes(int32_t* params_size, int32_t* result_size);
+
+/* Persistent-grid size (resident workgroups) chosen for the handle's device. */
+int32_t mpcqp_handle_slots(mpcqp_handle* h);
+
+/* Threads per instance workgroup of the solve kernel. */
+int32_t mpcqp_solve_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,65 @@
+/*
+ * mpc_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU (binary64) restatement of the reference hot path, used as the parity checker by tests/,
+ * __graft_entry__.smoke() and as bench.py's cpu_baseline ("port").  The product path never
+ * links or calls this code.
+ *
+ * Parity status: the formulation follows src/a1_cpp/src/ConvexMpc.cpp and
+ * src/a1_cpp/src/A1RobotControl.cpp line by line.  The QP solver restates OSQP 0.6.x
+ * (third-party, cloned unpinned in docker/Dockerfile:74-98, not vendored in the reference and
+ * not buildable here).  No reference test pins results at that boundary, so the OSQP iterate
+ * sequence is "parity unpinned" (see DESIGN.md §Oracle).
+ */
+#ifndef MPC_ORACLE_H_
+#define MPC_ORACLE_H_
+
+#include "../include/mpcqp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Robot-state view of A1CtrlStates / Go1CtrlStates fields read by compute_grf's MPC branch
+ * (A1RobotControl.cpp:446-514).  Matrices are row-major; foot_pos_abs is [leg][xyz]. */
+typedef struct orc_robot_state {
+  double root_euler[3], root_pos[3], root_ang_vel[3], root_lin_vel[3];
+  double root_rot_mat[9];
+  double root_euler_d[3], root_pos_d[3], root_ang_vel_d[3], root_lin_vel_d[3];
+  double foot_pos_abs[12];
+  double robot_mass, trunk_inertia[9];
+  double mu, fz_min, fz_max, mpc_dt;
+  int32_t contacts[4];
+} orc_robot_state;
+
+/* Per-check trace of one solve (iteration, residuals, rho) for parity diagnostics. */
+typedef struct orc_trace_entry {
+  int32_t iter, rho_updated;
+  double pri_res, dua_res, eps_prim, eps_dual, rho;
+} orc_trace_entry;
+
+/* compute_grf MPC-branch input assembly (A1RobotControl.cpp:446-514) → problem record.
+ * `rec` must hold mpcqp_record_size(N) doubles. */
+void orc_assemble_compute_grf(const orc_robot_state* s, int32_t N, double* rec);
+
+/* test_mpc.cpp:15-122 hand-set stance → problem record (feet shift by -v_d*dt per step). */
+void orc_assemble_test_mpc(int32_t N, double* rec, double q_weights[13], double r_weights[12]);
+
+/* ConvexMpc::calculate_qp_mats restatement.  P is full symmetric row-major [n][n],
+ * q [n], l/u [m], Acon row-major dense constraint matrix [m][n] (may be NULL). */
+int32_t orc_build_qp(const mpcqp_params* prm, const double* rec, double* P, double* q,
+                     double* l, double* u, double* Acon);
+
+/* OSQP 0.6 restatement on the QP built from `rec`; cold start.  sol: [12N] or NULL.
+ * trace: optional array of max_trace entries; *n_trace receives the count. */
+int32_t orc_solve(const mpcqp_params* prm, const double* rec, mpcqp_result* res, double* sol,
+                  orc_trace_entry* trace, int32_t max_trace, int32_t* n_trace);
+
+/* Batch over `nthreads` POSIX threads (static contiguous partition).  sols may be NULL. */
+int32_t orc_solve_batch(const mpcqp_params* prm, const double* recs, int32_t batch,
+                        mpcqp_result* res, double* sols, int32_t nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,84 @@
+"""TEST INFRASTRUCTURE — an independent numpy restatement of ConvexMpc's formulation and a KKT
+verifier for the QP.  Written separately from oracle/mpc_oracle.c so the two cross-check each
+other (the reference itself cannot be compiled here: Eigen/OSQP/ROS absent).
+
+Formulation: src/a1_cpp/src/ConvexMpc.cpp:7-245 (A_c :110-130, B_c :132-143, Euler
+discretization :145-156, A_qp/B_qp :184-202, H :207-211, gradient :215-217, bounds :223-245).
+"""
+import numpy as np
+
+REC_X0, REC_EULER, REC_ROT, REC_INERTIA = 0, 13, 16, 25
+REC_MASS, REC_MU, REC_FZMIN, REC_FZMAX, REC_DT, REC_CONTACTS, REC_XREF = 34, 35, 36, 37, 38, 39, 44
+INF = 1e30
+
+
+def skew(v):
+    return np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
+
+
+def condensed_qp(rec, N, q_w, r_w):
+    dt = rec[REC_DT]
+    yaw = rec[REC_EULER + 2]
+    Ac = np.zeros((13, 13))
+    Ac[0:3, 6:9] = [[np.cos(yaw), np.sin(yaw), 0], [-np.sin(yaw), np.cos(yaw), 0], [0, 0, 1]]
+    Ac[3:6, 9:12] = np.eye(3)
+    Ac[11, 12] = 1.0
+    Ad = np.eye(13) + Ac * dt
+    R = rec[REC_ROT:REC_ROT + 9].reshape(3, 3)
+    Ib = rec[REC_INERTIA:REC_INERTIA + 9].reshape(3, 3)
+    Iw_inv = np.linalg.inv(R @ Ib @ R.T)
+    mass = rec[REC_MASS]
+    feet = rec[REC_XREF + 13 * N: REC_XREF + 25 * N].reshape(N, 4, 3)
+    Bd = []
+    for i in range(N):
+        Bc = np.zeros((13, 12))
+        for leg in range(4):
+            Bc[6:9, 3 * leg:3 * leg + 3] = Iw_inv @ skew(feet[i, leg])
+            Bc[9:12, 3 * leg:3 * leg + 3] = np.eye(3) / mass
+        Bd.append(Bc * dt)
+    Aqp = np.zeros((13 * N, 13))
+    Bqp = np.zeros((13 * N, 12 * N))
+    P = np.eye(13)
+    for i in range(N):
+        P = P @ Ad
+        Aqp[13 * i:13 * i + 13] = P
+        for j in range(i + 1):
+            Bqp[13 * i:13 * i + 13, 12 * j:12 * j + 12] = np.linalg.matrix_power(Ad, i - j) @ Bd[j]
+    Q = np.diag(2 * np.tile(q_w, N))
+    Rm = np.diag(2 * np.tile(r_w, N))
+    H = Bqp.T @ Q @ Bqp + Rm
+    x0 = rec[REC_X0:REC_X0 + 13]
+    xref = rec[REC_XREF:REC_XREF + 13 * N]
+    g = Bqp.T @ Q @ (Aqp @ x0 - xref)
+    mu = rec[REC_MU]
+    C = np.zeros((20 * N, 12 * N))
+    blk = np.array([[1, 0, mu], [1, 0, -mu], [0, 1, mu], [0, 1, -mu], [0, 0, 1]])
+    lo, hi = [], []
+    for f in range(4 * N):
+        C[5 * f:5 * f + 5, 3 * f:3 * f + 3] = blk
+        c = 1.0 if rec[REC_CONTACTS + f % 4] != 0 else 0.0
+        lo += [0, -INF, 0, -INF, rec[REC_FZMIN] * c]
+        hi += [INF, 0, INF, 0, rec[REC_FZMAX] * c]
+    return H, g, C, np.array(lo), np.array(hi)
+
+
+def kkt_residuals(H, g, C, lo, hi, x, tol_active=1e-6):
+    """Return (stationarity, primal violation) for x using a nonnegative-LS multiplier fit."""
+    from scipy.optimize import lsq_linear
+    Cx = C @ x
+    prim = max(0.0, float(np.max(np.maximum(lo - Cx, Cx - hi))))
+    # multipliers y with sign constraints: y_i >= 0 at upper-active, <= 0 at lower-active, 0 else
+    act_lo = (Cx - lo) <= tol_active * np.maximum(1.0, np.abs(lo))
+    act_hi = (hi - Cx) <= tol_active * np.maximum(1.0, np.abs(hi))
+    lb = np.where(act_lo & ~act_hi, -np.inf, 0.0)
+    ub = np.where(act_hi & ~act_lo, np.inf, 0.0)
+    both = act_lo & act_hi
+    lb[both], ub[both] = -np.inf, np.inf
+    fr = (lb != 0) | (ub != 0)
+    r = -(H @ x + g)
+    if fr.any():
+        sol = lsq_linear(C[fr].T, r, bounds=(lb[fr], ub[fr]))
+        stat = float(np.max(np.abs(C[fr].T @ sol.x - r)))
+    else:
+        stat = float(np.max(np.abs(r)))
+    return stat, prim
