@@ -224,9 +224,10 @@ __device__ void condense(Smem<N>& sm, const mpcqp_params& p, double* __restrict_
           // B_c[6:9, 3l:3l+3] = I_w^-1 skew(foot_l)  (Utils.cpp:35-41), B_d = B_c dt
           const int leg = c / 3, cc = c % 3;
           const double* fp = rec + Dm::feet + 12 * k + 3 * leg;
-          const double sk0 = cc == 0 ? 0.0 : cc == 1 ? fp[2] : -fp[1];
-          const double sk1 = cc == 0 ? -fp[2] : cc == 1 ? 0.0 : fp[0];
-          const double sk2 = cc == 0 ? fp[1] : cc == 1 ? -fp[0] : 0.0;
+          // column cc of skew(v) = [[0,-v2,v1],[v2,0,-v0],[-v1,v0,0]]
+          const double sk0 = cc == 0 ? 0.0 : cc == 1 ? -fp[2] : fp[1];
+          const double sk1 = cc == 0 ? fp[2] : cc == 1 ? 0.0 : -fp[0];
+          const double sk2 = cc == 0 ? -fp[1] : cc == 1 ? fp[0] : 0.0;
           const double* iw = C.Iwinv + (r - 6) * 3;
           double s = 0.0;
           s += iw[0] * sk0;
