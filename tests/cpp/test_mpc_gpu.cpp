@@ -1,0 +1,118 @@
+// C++ port of the reference harness src/a1_cpp/src/test/test_mpc.cpp:14-162, driven through the
+// drop-in shim (include/mpcqp_robot_control.hpp) instead of Eigen/OsqpEigen.  Same hand-set
+// stance, same call sequence (ConvexMpc ctor/reset, A_c from the horizon-average euler, B per step
+// with shifted feet, calculate_qp_mats), then the GPU solve.  Prints machine-readable lines that
+// tests/test_cpp_shim.py compares with the CPU oracle.
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/mpcqp_robot_control.hpp"
+
+struct Vec {  // Eigen::VectorXd stand-in for the test (operator[])
+  double v[300] = {0};
+  double& operator[](int i) { return v[i]; }
+  const double& operator[](int i) const { return v[i]; }
+};
+struct Mat {  // Eigen::Matrix stand-in (operator()(r,c)), row-major up to 3x4
+  double a[3][4] = {{0}};
+  double& operator()(int r, int c) { return a[r][c]; }
+  const double& operator()(int r, int c) const { return a[r][c]; }
+};
+struct State {  // the A1CtrlStates fields test_mpc touches
+  double robot_mass = 0;
+  Mat a1_trunk_inertia, root_rot_mat, foot_pos_rel, foot_pos_abs_mpc, foot_pos_abs;
+  Vec root_euler, root_pos, root_ang_vel, root_lin_vel, root_euler_d, root_pos_d, root_ang_vel_d, root_lin_vel_d,
+      root_lin_vel_d_world, mpc_states, mpc_states_d;
+  bool contacts[4] = {false, false, false, false};
+};
+
+int main() {
+  constexpr int PLAN_HORIZON = 10;
+  State state;
+  state.robot_mass = 15;  // :18
+  state.a1_trunk_inertia(0, 0) = 0.0158533;
+  state.a1_trunk_inertia(1, 1) = 0.0377999;
+  state.a1_trunk_inertia(2, 2) = 0.0456542;
+  for (int i = 0; i < 3; ++i) state.root_rot_mat(i, i) = 1.0;  // :25-30, all-zero angles
+  state.root_pos[2] = 0.15;                                     // :32
+  const double fx[4] = {0.17, 0.17, -0.17, -0.17}, fy[4] = {0.15, -0.15, 0.15, -0.15};
+  for (int l = 0; l < 4; ++l) {  // :39-41
+    state.foot_pos_rel(0, l) = fx[l];
+    state.foot_pos_rel(1, l) = fy[l];
+    state.foot_pos_rel(2, l) = -0.35;
+  }
+  state.contacts[0] = true;  // :43-46
+  state.contacts[2] = true;
+  const double dt = 0.0025;
+  Vec q_weights, r_weights;  // :50-60
+  const double q[13] = {1.0, 1.0, 1.0, 0.0, 0.0, 50.0, 0.0, 0.0, 1.0, 1.0, 1.0, 1.0, 0.0};
+  for (int i = 0; i < 13; ++i) q_weights[i] = q[i];
+  for (int i = 0; i < 12; ++i) r_weights[i] = 1e-6;
+  mpcqp_cpp::ConvexMpc<PLAN_HORIZON> mpc_solver(q_weights, r_weights);
+  mpc_solver.reset();
+  const double x0[13] = {state.root_euler[0], state.root_euler[1], state.root_euler[2], state.root_pos[0],
+                         state.root_pos[1], state.root_pos[2], state.root_ang_vel[0], state.root_ang_vel[1],
+                         state.root_ang_vel[2], state.root_lin_vel[0], state.root_lin_vel[1], state.root_lin_vel[2],
+                         -9.8};
+  for (int k = 0; k < 13; ++k) state.mpc_states[k] = x0[k];
+  for (int r = 0; r < 3; ++r) {  // :73
+    double acc = 0;
+    for (int c = 0; c < 3; ++c) acc += state.root_rot_mat(r, c) * state.root_lin_vel_d[c];
+    state.root_lin_vel_d_world[r] = acc;
+  }
+  for (int i = 0; i < PLAN_HORIZON; ++i) {  // :75-91
+    const double xr[13] = {state.root_euler_d[0], state.root_euler_d[1],
+                           state.root_euler[2] + state.root_ang_vel_d[2] * dt * (i + 1),
+                           state.root_pos[0] + state.root_lin_vel_d_world[0] * dt * (i + 1),
+                           state.root_pos[1] + state.root_lin_vel_d_world[1] * dt * (i + 1),
+                           state.root_pos[2] + state.root_lin_vel_d_world[1] * dt * (i + 1),
+                           state.root_ang_vel_d[0], state.root_ang_vel_d[1], state.root_ang_vel_d[2],
+                           state.root_lin_vel_d_world[0], state.root_lin_vel_d_world[1],
+                           state.root_lin_vel_d_world[2], -9.8};
+    for (int k = 0; k < 13; ++k) state.mpc_states_d[13 * i + k] = xr[k];
+  }
+  Vec avg;  // :94-101
+  for (int k = 0; k < 3; ++k)
+    avg[k] = (state.root_euler[k] + state.root_euler[k] + state.root_ang_vel_d[k] * dt * PLAN_HORIZON) /
+             (PLAN_HORIZON + 1);
+  mpc_solver.calculate_A_mat_c(avg);
+  state.foot_pos_abs_mpc = state.foot_pos_rel;  // :105
+  for (int i = 0; i < PLAN_HORIZON; i++) {      // :106-122
+    mpc_solver.calculate_B_mat_c(state.robot_mass, state.a1_trunk_inertia, state.root_rot_mat,
+                                 state.foot_pos_abs_mpc);
+    for (int l = 0; l < 4; ++l)
+      for (int r = 0; r < 3; ++r) state.foot_pos_abs_mpc(r, l) -= state.root_lin_vel_d[r] * dt;
+    mpc_solver.state_space_discretization(dt);
+  }
+  mpc_solver.calculate_qp_mats(state);  // :125
+  double hsum = 0, hmax = 0, gsum = 0;
+  for (double v : mpc_solver.hessian) { hsum += v; hmax = v > hmax ? v : hmax; }
+  for (double v : mpc_solver.gradient) gsum += v;
+  std::printf("HESSIAN_SUM %.17g\nHESSIAN_MAX %.17g\nGRADIENT_SUM %.17g\n", hsum, hmax, gsum);
+  std::printf("HESSIAN_00 %.17g\n", mpc_solver.hessian[0]);
+
+  // :131-151 solve (fresh solver, cold start) through the C ABI
+  mpcqp_result res;
+  mpcqp_cpp::throw_on(mpcqp_solve_batch_host(mpc_solver.handle(), mpc_solver.record().data(), 1, &res, nullptr),
+                      mpc_solver.handle(), "solve");
+  std::printf("STATUS %d ITERS %d RHO_UPDATES %d\n", res.status, res.iters, res.rho_updates);
+  // :153-157 print the 3x4 world-frame forces
+  for (int r = 0; r < 3; ++r) {
+    std::printf("ROW");
+    for (int l = 0; l < 4; ++l) std::printf(" %.17g", res.u0[3 * l + r]);
+    std::printf("\n");
+  }
+
+  // compute_grf (A1RobotControl.cpp:446-561) on the same stance, production assembly
+  state.foot_pos_abs = state.foot_pos_rel;
+  state.root_pos_d[2] = 0.15;
+  mpcqp_cpp::A1RobotControl ctrl(q_weights, r_weights);
+  Mat forces;
+  ctrl.compute_grf(state, dt, forces);
+  for (int r = 0; r < 3; ++r) {
+    std::printf("GRF");
+    for (int l = 0; l < 4; ++l) std::printf(" %.17g", forces(r, l));
+    std::printf("\n");
+  }
+  return 0;
+}

@@ -82,3 +82,58 @@ def kkt_residuals(H, g, C, lo, hi, x, tol_active=1e-6):
     else:
         stat = float(np.max(np.abs(r)))
     return stat, prim
+
+
+def ipm_qp(H, g, C, lo, hi, tol=1e-10, max_iter=200):
+    """Independent dense primal-dual interior-point solver (Mehrotra predictor-corrector) for
+        min 1/2 x'Hx + g'x  s.t.  lo <= Cx <= hi
+    Rows with lo == hi become equalities; +-1e30 bounds are dropped.  Returns x."""
+    n = H.shape[0]
+    eq = np.isclose(lo, hi, rtol=0, atol=0)
+    Ae, be = C[eq], lo[eq]
+    up = (~eq) & (hi < INF / 10)
+    dn = (~eq) & (lo > -INF / 10)
+    G = np.vstack([C[up], -C[dn]])
+    h = np.concatenate([hi[up], -lo[dn]])
+    p, me = G.shape[0], Ae.shape[0]
+    x = np.zeros(n)
+    s = np.maximum(h - G @ x, 1.0)
+    z = np.ones(p)
+    yv = np.zeros(me)
+    for _ in range(max_iter):
+        rd = H @ x + g + G.T @ z + Ae.T @ yv
+        rp = G @ x + s - h
+        re = Ae @ x - be
+        mu = s @ z / p
+        # scale-aware stop: iterating past this point only accumulates roundoff (W = z/s spans
+        # ~1e20 at the end and the reduced KKT solve loses accuracy)
+        dscale = 1.0 + np.max(np.abs(g)) + np.max(np.abs(H)) * np.max(np.abs(x))
+        pscale = 1.0 + np.max(np.abs(h)) + np.max(np.abs(G)) * np.max(np.abs(x))
+        if (np.max(np.abs(rd)) < tol * dscale and np.max(np.abs(rp)) < tol * pscale
+                and (not me or np.max(np.abs(re)) < tol * pscale) and mu < tol * dscale):
+            break
+
+        def solve(rc):
+            # Newton on H dx + G'dz + Ae'dy = -rd, G dx + ds = -rp, Ae dx = -re, Z ds + S dz = -rc.
+            # Eliminating ds, dz: (H + G'WG) dx + Ae'dy = -rd - G'((z rp - rc)/s),  W = Z/S
+            W = z / s
+            K = np.block([[H + G.T @ (W[:, None] * G), Ae.T], [Ae, np.zeros((me, me))]])
+            rhs = np.concatenate([-rd - G.T @ ((z * rp - rc) / s), -re])
+            sol = np.linalg.solve(K, rhs)
+            dx, dy = sol[:n], sol[n:]
+            ds = -rp - G @ dx
+            dz = -(rc + z * ds) / s
+            return dx, dy, ds, dz
+
+        def step_len(v, dv):
+            neg = dv < 0
+            return min(1.0, float(np.min(-v[neg] / dv[neg]))) if neg.any() else 1.0
+
+        dx, dy, ds, dz = solve(s * z)           # affine: rc = s*z  (target s*z -> 0)
+        a = min(step_len(s, ds), step_len(z, dz))
+        mu_aff = (s + a * ds) @ (z + a * dz) / p
+        sigma = (mu_aff / mu) ** 3
+        dx, dy, ds, dz = solve(s * z + ds * dz - sigma * mu)
+        a = 0.99 * min(step_len(s, ds), step_len(z, dz))
+        x, yv, s, z = x + a * dx, yv + a * dy, s + a * ds, z + a * dz
+    return x

@@ -1,0 +1,56 @@
+"""The C++ drop-in shim (include/mpcqp_robot_control.hpp) running the reference's own harness
+(test_mpc.cpp, ported in tests/cpp/test_mpc_gpu.cpp) on the GPU, checked against the oracle."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import mpcqp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(REPO, "tests", "cpp", "build", "test_mpc_gpu")
+
+
+@pytest.mark.gpu
+def test_cpp_test_mpc_harness(oracle):
+    if not os.path.exists(EXE):
+        subprocess.run(["make", "-C", os.path.join(REPO, "tests", "cpp")], check=True)
+    out = subprocess.run([EXE], check=True, capture_output=True, text=True, timeout=120).stdout
+    kv = {}
+    rows, grf = [], []
+    for line in out.splitlines():
+        parts = line.split()
+        if parts[0] == "ROW":
+            rows.append([float(x) for x in parts[1:]])
+        elif parts[0] == "GRF":
+            grf.append([float(x) for x in parts[1:]])
+        elif parts[0] == "STATUS":
+            kv["status"], kv["iters"], kv["rho_updates"] = int(parts[1]), int(parts[3]), int(parts[5])
+        else:
+            kv[parts[0]] = float(parts[1])
+    rec, q, r = mpcqp.assemble_test_mpc(10)
+    op = oracle.default_params(10, q=list(q), r=list(r))
+    P, g, l, u, A = oracle.build_qp(op, rec)
+    assert abs(kv["HESSIAN_SUM"] - P.sum()) <= 1e-12 * np.abs(P).sum()
+    assert abs(kv["HESSIAN_MAX"] - P.max()) <= 1e-12 * np.abs(P).max()
+    assert abs(kv["GRADIENT_SUM"] - g.sum()) <= 1e-12 * max(np.abs(g).sum(), 1e-300) + 1e-18
+    ref, _ = oracle.solve(op, rec)
+    u0 = np.array(rows).T.reshape(12)  # [leg][xyz]
+    assert np.max(np.abs(u0 - ref["u0"])) <= 1e-4 * max(np.max(np.abs(ref["u0"])), 1)
+    assert (kv["status"], kv["iters"], kv["rho_updates"]) == (int(ref["status"]), int(ref["iters"]), int(ref["rho_updates"]))
+    # compute_grf (production assembly) on the same stance
+    s = oracle.RobotState()
+    s.root_pos[:] = [0, 0, 0.15]
+    s.root_rot_mat[:] = [1, 0, 0, 0, 1, 0, 0, 0, 1]
+    s.root_pos_d[:] = [0, 0, 0.15]
+    s.foot_pos_abs[:] = [0.17, 0.15, -0.35, 0.17, -0.15, -0.35, -0.17, 0.15, -0.35, -0.17, -0.15, -0.35]
+    s.robot_mass = 15
+    s.trunk_inertia[:] = [0.0158533, 0, 0, 0, 0.0377999, 0, 0, 0, 0.0456542]
+    s.mu, s.fz_min, s.fz_max, s.mpc_dt = 0.3, 0.0, 180.0, 0.0025
+    s.contacts[:] = [1, 0, 1, 0]
+    rec2 = oracle.assemble_compute_grf(s, 10)
+    ref2, _ = oracle.solve(op, rec2)
+    f = np.array(grf)  # 3x4 body frame
+    fr = np.array(ref2["f_body"]).reshape(4, 3).T
+    assert np.max(np.abs(f - fr)) <= 1e-4 * max(np.max(np.abs(fr)), 1)

@@ -1,0 +1,62 @@
+"""Multi-rank path on CPU: world_size-2 gloo, contiguous robot shards + all-gather of forces.
+
+The per-rank solve here is the CPU oracle standing in for the device solve (tests only); the code
+under test is mpcqp.distributed (shard_range / allgather_forces), used by bench.py on RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import mpcqp
+from mpcqp.distributed import allgather_forces, shard_range
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, total, out_dir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "oracle")]
+    import pyoracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    st = mpcqp.synthetic_go1(total, seed=123, gait="trot")
+    recs = mpcqp.assemble_compute_grf(st, 10)
+    b, e = shard_range(total, world, rank)
+    res = pyoracle.solve_batch(pyoracle.default_params(10), recs[b:e], nthreads=1)
+    local = torch.from_numpy(np.ascontiguousarray(res["u0"]))
+    full = allgather_forces(local, total)
+    np.save(os.path.join(out_dir, f"rank{rank}.npy"), full.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total", [8, 7])
+def test_sharded_allgather_matches_single_rank(oracle, tmp_path, total):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), total, str(tmp_path)), nprocs=world, join=True)
+    st = mpcqp.synthetic_go1(total, seed=123, gait="trot")
+    ref = oracle.solve_batch(oracle.default_params(10), mpcqp.assemble_compute_grf(st, 10), nthreads=2)
+    for r in range(world):
+        got = np.load(tmp_path / f"rank{r}.npy")
+        np.testing.assert_array_equal(got, ref["u0"])
+
+
+def test_shard_range_partitions():
+    for total in (0, 1, 7, 8, 65536, 65537):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [e - b for b, e in spans]
+            assert max(sizes) - min(sizes) <= 1

@@ -1,0 +1,78 @@
+"""GPU path vs committed golden vectors, and size-independent properties at the BASELINE sizes
+(C2: 4096 trot, C5: 8192 mixed gait + random mu, C3 shard: 8192 per GPU)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import mpcqp
+from gpu_helpers import rel_err_u0, solve_gpu
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SETS = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+@pytest.mark.parametrize("path", SETS, ids=[os.path.basename(p) for p in SETS])
+def test_gpu_matches_golden(path):
+    d = np.load(path)
+    p = mpcqp.default_params(10, q_weights=d["q_weights"], r_weights=d["r_weights"])
+    with mpcqp.MpcQpSolver(p) as s:
+        got, sol, _ = solve_gpu(s, d["records"])
+    assert np.all(rel_err_u0(got["u0"], d["u0"]) <= 1e-4)
+    np.testing.assert_array_equal(got["status"], d["status"])
+    np.testing.assert_array_equal(got["iters"], d["iters"])
+    np.testing.assert_array_equal(got["rho_updates"], d["rho_updates"])
+    full = np.max(np.abs(sol - d["x"]), axis=1) / np.maximum(np.max(np.abs(d["x"]), axis=1), 1.0)
+    assert np.all(full <= 1e-4)
+
+
+def _friction_ok(recs, sol, tol=0.25):
+    B = recs.shape[0]
+    mu = recs[:, mpcqp._lib.REC_MU][:, None]
+    c = np.tile(recs[:, mpcqp._lib.REC_CONTACTS:mpcqp._lib.REC_CONTACTS + 4] != 0, (1, 10))
+    x = sol.reshape(B, -1, 3)
+    return (np.all(np.abs(x[..., 0]) <= mu * x[..., 2] + tol) and np.all(np.abs(x[..., 1]) <= mu * x[..., 2] + tol)
+            and np.all(x[..., 2] >= -tol) and np.all(x[..., 2] <= 180 * c + tol))
+
+
+@pytest.mark.parametrize("B,gait,mixed_mu,seed", [(4096, "trot", False, 1000), (8192, "mixed", True, 4000),
+                                                  (8192, "trot", False, 2000)])
+def test_fullsize_properties(oracle, B, gait, mixed_mu, seed):
+    st = mpcqp.synthetic_go1(B, seed=seed, gait=gait, mixed_mu=mixed_mu)
+    recs = mpcqp.assemble_compute_grf(st, 10)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+        got, sol, _ = solve_gpu(s, recs)
+        got2, sol2, _ = solve_gpu(s, recs)
+    # idempotence / determinism: identical bits on a re-run
+    np.testing.assert_array_equal(sol, sol2)
+    np.testing.assert_array_equal(got["iters"], got2["iters"])
+    # every robot solved, forces inside the friction pyramid and fz bounds (OSQP tolerance)
+    assert np.all(got["status"] == mpcqp._lib.STATUS_SOLVED)
+    assert _friction_ok(recs, sol)
+    # swing legs carry no force at step 0
+    swing = recs[:, mpcqp._lib.REC_CONTACTS:mpcqp._lib.REC_CONTACTS + 4] == 0
+    assert np.all(np.abs(got["u0"].reshape(B, 4, 3)[swing]) <= 1e-3)
+    # f_body = R^T u0 per leg
+    R = recs[:, mpcqp._lib.REC_ROT:mpcqp._lib.REC_ROT + 9].reshape(B, 3, 3)
+    fb = np.einsum("bji,blj->bli", R, got["u0"].reshape(B, 4, 3)).reshape(B, 12)
+    np.testing.assert_allclose(got["f_body"], fb, rtol=0, atol=1e-9)
+    # a random subset against the oracle (schedule-identical parity)
+    idx = np.random.default_rng(seed).choice(B, 96, replace=False)
+    ref = oracle.solve_batch(oracle.default_params(10), recs[idx], nthreads=8)
+    assert np.all(rel_err_u0(got["u0"][idx], ref["u0"]) <= 1e-4)
+    np.testing.assert_array_equal(got["iters"][idx], ref["iters"])
+
+
+def test_batch_order_independence():
+    """Results do not depend on batch composition / workgroup placement."""
+    st = mpcqp.synthetic_go1(512, seed=8, gait="mixed", mixed_mu=True)
+    recs = mpcqp.assemble_compute_grf(st, 10)
+    perm = np.random.default_rng(0).permutation(512)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+        a, sa, _ = solve_gpu(s, recs)
+        b, sb, _ = solve_gpu(s, recs[perm])
+        c, sc, _ = solve_gpu(s, recs[:1])
+    np.testing.assert_array_equal(sa[perm], sb)
+    np.testing.assert_array_equal(sa[:1], sc)
