@@ -273,7 +273,9 @@ __device__ void condense(Smem<N>& sm, const mpcqp_params& p, double* __restrict_
 #pragma unroll
     for (int q = 0; q < EP; ++q) {
       const int e = t + q * NT;
-      if (e < ND * ND * (k + 1)) {
+      // diagonal block (j == k): only a <= cc, mirrored, so each location has exactly one writer
+      // (the two triangles of B_k' S_k B_k round differently)
+      if (e < ND * ND * (k + 1) && !((e / ND) / ND == k && (e / ND) % ND > e % ND)) {
         const int rr = e / ND, cc = e % ND;
         const int j = rr / ND, a = rr % ND;
         double s = 0.0;

@@ -28,13 +28,15 @@ def test_gpu_matches_golden(path):
     assert np.all(full <= 1e-4)
 
 
-def _friction_ok(recs, sol, tol=0.25):
+def _pyramid_violation(recs, sol):
+    """max over rows of dist(Ax, [l, u]) per robot (friction pyramid + fz bounds)."""
     B = recs.shape[0]
     mu = recs[:, mpcqp._lib.REC_MU][:, None]
     c = np.tile(recs[:, mpcqp._lib.REC_CONTACTS:mpcqp._lib.REC_CONTACTS + 4] != 0, (1, 10))
     x = sol.reshape(B, -1, 3)
-    return (np.all(np.abs(x[..., 0]) <= mu * x[..., 2] + tol) and np.all(np.abs(x[..., 1]) <= mu * x[..., 2] + tol)
-            and np.all(x[..., 2] >= -tol) and np.all(x[..., 2] <= 180 * c + tol))
+    fx, fy, fz = x[..., 0], x[..., 1], x[..., 2]
+    v = np.stack([-(fx + mu * fz), fx - mu * fz, -(fy + mu * fz), fy - mu * fz, -fz, fz - 180 * c])
+    return np.max(np.maximum(v, 0.0), axis=(0, 2))
 
 
 @pytest.mark.parametrize("B,gait,mixed_mu,seed", [(4096, "trot", False, 1000), (8192, "mixed", True, 4000),
@@ -48,12 +50,14 @@ def test_fullsize_properties(oracle, B, gait, mixed_mu, seed):
     # idempotence / determinism: identical bits on a re-run
     np.testing.assert_array_equal(sol, sol2)
     np.testing.assert_array_equal(got["iters"], got2["iters"])
-    # every robot solved, forces inside the friction pyramid and fz bounds (OSQP tolerance)
+    # every robot solved; friction pyramid / fz bounds hold up to the robot's own primal residual
+    # (z is projected onto [l, u], so dist(Ax, [l, u]) <= ||Ax - z||_inf = pri_res < eps_prim)
     assert np.all(got["status"] == mpcqp._lib.STATUS_SOLVED)
-    assert _friction_ok(recs, sol)
-    # swing legs carry no force at step 0
+    assert np.all(_pyramid_violation(recs, sol) <= got["pri_res"] + 1e-9)
+    # swing legs carry no force at step 0 (|f| <= (1 + mu) pri_res)
     swing = recs[:, mpcqp._lib.REC_CONTACTS:mpcqp._lib.REC_CONTACTS + 4] == 0
-    assert np.all(np.abs(got["u0"].reshape(B, 4, 3)[swing]) <= 1e-3)
+    bound = ((1 + recs[:, mpcqp._lib.REC_MU]) * got["pri_res"] + 1e-9)[:, None, None]
+    assert np.all((np.abs(got["u0"].reshape(B, 4, 3)) <= bound)[swing])
     # f_body = R^T u0 per leg
     R = recs[:, mpcqp._lib.REC_ROT:mpcqp._lib.REC_ROT + 9].reshape(B, 3, 3)
     fb = np.einsum("bji,blj->bli", R, got["u0"].reshape(B, 4, 3)).reshape(B, 12)
