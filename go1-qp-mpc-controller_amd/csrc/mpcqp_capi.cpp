@@ -18,7 +18,7 @@ struct mpcqp_handle {
   mpcqp_params p;
   int device = 0;
   int slots = 0;             // resident workgroups per device (occupancy x CUs), informational
-  double* work = nullptr;    // per-instance 128x128 binary64 workspace (scaled Hessian)
+  double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
   // host wrapper staging
   double* d_recs = nullptr;
@@ -132,7 +132,7 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
     if (e == hipSuccess) e = hipFree(h->work);
     h->work = nullptr;
     h->work_cap = 0;
-    if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * (size_t)mpcqp::NP * mpcqp::NP * batch);
+    if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * mpcqp::workspace_doubles(h->p.horizon) * batch);
     if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
     h->work_cap = batch;
   }
@@ -257,11 +257,11 @@ int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {
   if (e == hipSuccess) e = hipFree(h->work);
   h->work = nullptr;
   h->work_cap = 0;
-  if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * (size_t)mpcqp::NP * mpcqp::NP * batch);
+  if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * mpcqp::workspace_doubles(h->p.horizon) * batch);
   if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
   h->work_cap = batch;
   return MPCQP_OK;
 }
-int32_t mpcqp_solve_threads(void) { return mpcqp::solve_threads(); }
+int32_t mpcqp_solve_threads(int32_t horizon) { return mpcqp::solve_threads(horizon); }
 
 }  // extern "C"

@@ -1,19 +1,25 @@
 // mpcqp_kernels.hip — CDNA4 (gfx950) kernels of the batched convex-MPC QP engine.
 //
-// One 512-thread workgroup (8 waves, 2 per SIMD) solves one robot instance; the hardware
-// dispatcher back-fills CUs as instances finish (iteration counts differ).  Per instance:
+// One workgroup solves one robot.  Its threads form one 16-lane group per FOOT (4 per horizon
+// step; 40 groups = 640 threads = 10 waves at N = 10).  Group f owns, in registers, the 3 rows of
+// the KKT matrix / its inverse that belong to foot f's force (fx, fy, fz), split in 16 column
+// tiles of BC = 8; lanes 0-4 of the group own the foot's 5 friction-pyramid rows, lanes 5-7 its 3
+// variables.  Per robot:
 //
 //   1. condensation (ConvexMpc::calculate_qp_mats, src/a1_cpp/src/ConvexMpc.cpp:158-245)
-//        S_k = Q + A_d' S_{k+1} A_d  (backward),  B_qp(k,j) = A_d B_qp(k-1,j)  (forward),
-//        H[block j][block k] = B_qp(k,j)' S_k B_d(k)  (j <= k),  g_j = sum_k B_qp(k,j)' Q e_k,
-//      written once to a per-instance HBM/L2 workspace (H is needed again at every rho refactor);
-//   2. OSQP 0.6 Ruiz equilibration (scaling.c) on H held in REGISTERS: every thread owns a
-//      4x8 tile of the 128x128 (padded) matrix, tiles row-reduced with 16-lane shuffles;
-//   3. K = P~ + sigma I + A~' diag(rho) A~ and its inverse by in-register Gauss-Jordan
-//      (pivot row/column broadcast through a double-buffered LDS line, one barrier per pivot);
-//   4. ADMM (osqp.c) with x~ = K^-1 rhs as a register-tile mat-vec + 16-lane reduce-scatter;
-//      the friction-pyramid rows are handled per foot (5 rows x 3 vars) by wave 0, with
-//      termination checks / adaptive rho every 25 iterations exactly as OSQP 0.6.
+//        S_k = Q + A_d' S_{k+1} A_d (backward), B_qp(k,j) = A_d B_qp(k-1,j) (forward in LDS),
+//        H_jk = B_qp(k,j)' S_k B_d(k) (j <= k), g_j = sum_k B_qp(k,j)' Q (A^{k+1} x0 - x_ref_k);
+//      H goes to a per-robot HBM/L2 workspace (it is re-read at every rho refactor);
+//   2. OSQP 0.6 Ruiz equilibration (scaling.c) on P held in registers; column norms = row norms
+//      of the symmetric tiles, reduced inside each 16-lane group with DPP;
+//   3. K = P~ + sigma I + A~' diag(rho) A~ and its inverse by block Gauss-Jordan with the foot's
+//      3x3 diagonal block as pivot (one barrier per foot);
+//   4. ADMM (osqp.c): x~ = K^-1 rhs is a register-tile mat-vec + 16-lane DPP all-reduce that
+//      lands x~ of foot f in group f, where the relaxation / projection / dual update and the
+//      next right-hand side are computed lane-parallel — ONE barrier per iteration; every 25
+//      iterations the termination test and adaptive rho run redundantly in every thread on
+//      workgroup-reduced norms (exactly OSQP 0.6's tests, see oracle/mpc_oracle.c);
+//   5. unscaling and compute_grf's extraction f_i = R^T u0[3i:3i+3] with its NaN guard.
 //
 // Arithmetic is binary64 throughout (the reference is double everywhere).
 #include <hip/hip_runtime.h>
@@ -36,24 +42,30 @@ struct Dim {
   static constexpr int n = ND * N, m = CD * N, nf = 4 * N, ns = SD * N;
   static constexpr int rec = MPCQP_REC_SIZE(N);
   static constexpr int feet = MPCQP_REC_FEET(N);
+  static constexpr int BC = (n + 15) / 16;  // columns per thread
+  static constexpr int NP = 16 * BC;        // padded column count
+  static constexpr int NT = 16 * nf;        // threads: one 16-lane group per foot
+  static constexpr int NW = NT / 64;        // waves
 };
 
-// LDS image of one instance.
+// LDS image of one robot.
 template <int N>
 struct Smem {
   using Dm = Dim<N>;
   double rec[Dm::rec];
-  double qt[Dm::n], D[Dm::n], Dinv[Dm::n], E[Dm::m], Einv[Dm::m], lo[Dm::m], hi[Dm::m];
-  double A9[Dm::nf][9];  // A~ per foot: {ax0, az0, ax1, az1, ay2, az2, ay3, az3, az4}
-  double BD[Dm::nf][9];  // (A~' diag(rho) A~) 3x3 block per foot, row-major
-  double rho_v[Dm::m], rho_inv[Dm::m];
+  // constraint rows (owned by lanes 0-4 of the foot's group)
+  double z[Dm::m], y[Dm::m], lo[Dm::m], hi[Dm::m], rho_v[Dm::m], rho_inv[Dm::m];
+  double am[Dm::m], az[Dm::m];  // A~ row: coefficient on the row's main variable / on fz
+  double E[Dm::m], Einv[Dm::m];
   int ctype[Dm::m];
-  alignas(16) double rhs[NP];
-  alignas(16) double xt[NP];
-  double X[Dm::n], Z[Dm::m], Y[Dm::m], PX[Dm::n];
-  alignas(16) double gj[2][2][NP];
-  double cst[8];  // 0: c, 1: cinv, 2: rho, 3: c_temp
-  int ctl[8];     // 0: instance, 1: done flag, 2: refactor flag, 3: status
+  // variables (owned by lanes 5-7)
+  double x[Dm::n], px[Dm::n], qt[Dm::n], D[Dm::n], Dinv[Dm::n], xrhs[Dm::n];
+  double BD[Dm::n][3];  // (A~' diag(rho) A~) row of each variable (3x3 block per foot)
+  alignas(16) double rhs[2][Dm::NP];  // KKT right-hand side, double-buffered by iteration parity
+  alignas(16) double Dt[Dm::NP];
+  double red[2][Dm::NW][16];              // workgroup reductions (double-buffered)
+  double info[Dm::NW][16];                // per-wave maxima of the termination / rho norms
+  double cst[4];                          // 0: c, 1: cinv
   union U {
     struct C {
       double S[N][SD * SD];
@@ -65,22 +77,20 @@ struct Smem {
       double a[SD];
       double w[SD];
     } c;
-    struct R {
-      alignas(16) double Dt[NP];
-      double Et[Dm::m];
-      double colP[NP];
-      double red[64];
-    } r;
+    struct G {  // block Gauss-Jordan broadcast lines (double-buffered)
+      alignas(16) double r[2][3][Dm::NP];  // P^-1 * pivot rows
+      double c[2][Dm::n][3];               // pivot columns
+      double p[2][9];                      // P^-1 (raw pivot block before phase A ends)
+    } g;
   } u;
 };
 
-// Returns v unchanged but opaque to the optimizer: values derived from it are recomputed where
-// used instead of being hoisted out of the ADMM loop (which exhausts the VGPR file).
+// Returns v unchanged but opaque to the optimizer, so values derived from it are recomputed in
+// the loop instead of being hoisted (and held live) across the whole ADMM loop.
 __device__ __forceinline__ int opaque(int v) {
   asm volatile("" : "+v"(v));
   return v;
 }
-
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 __device__ __forceinline__ double dabs(double a) { return a < 0 ? -a : a; }
@@ -89,63 +99,81 @@ __device__ __forceinline__ double limit_scaling(double d) {
   return d > MAX_SCALING ? MAX_SCALING : d;
 }
 
-// ---- 16-lane reductions (a lane group shares one tile row: t = tr*16 + tc) ------------------
-// Reduce-scatter: returns the reduction of v[row] for row = tc >> (4 - log2 BR) (lane groups
-// of 16/BR lanes hold the same row).
-template <int BR, bool MAX>
-__device__ __forceinline__ double rs16(double (&v)[BR], int tc) {
-  static_assert(BR == 1 || BR == 2 || BR == 4 || BR == 8, "BR must be a power of two <= 8");
-  constexpr int L = BR == 1 ? 0 : BR == 2 ? 1 : BR == 4 ? 2 : 3;
-  double a[BR];
-#pragma unroll
-  for (int i = 0; i < BR; ++i) a[i] = v[i];
-#pragma unroll
-  for (int s = 0; s < L; ++s) {
-    const int mask = 8 >> s;
-    const int half = BR >> (s + 1);
-    const bool up = (tc & mask) != 0;
-#pragma unroll
-    for (int i = 0; i < half; ++i) {
-      double send = up ? a[i] : a[i + half];
-      double keep = up ? a[i + half] : a[i];
-      double got = __shfl_xor(send, mask);
-      a[i] = MAX ? dmax(keep, got) : keep + got;
-    }
-  }
-  double r = a[0];
-#pragma unroll
-  for (int mask = 8 >> L; mask >= 1; mask >>= 1) {
-    double got = __shfl_xor(r, mask);
-    r = MAX ? dmax(r, got) : r + got;
-  }
-  return r;
+// ---- cross-lane helpers ----------------------------------------------------------------------
+// DPP move of a double inside a 16-lane row.  CTRL: 0x140 row_mirror (i <-> 15-i),
+// 0x141 row_half_mirror (i <-> 7-i in each half), 0x4E quad_perm xor 2, 0xB1 quad_perm xor 1.
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
 }
-
-// wave-wide (64-lane) all-reduce
+// 16-lane all-reduce; the four pairings generate the whole group and every step adds the same two
+// operands on both partners, so all 16 lanes end with bitwise-identical results.
+__device__ __forceinline__ double g16_sum(double v) {
+  v = v + dpp<0x140>(v);
+  v = v + dpp<0x141>(v);
+  v = v + dpp<0x4E>(v);
+  v = v + dpp<0xB1>(v);
+  return v;
+}
+__device__ __forceinline__ double g16_max(double v) {
+  v = dmax(v, dpp<0x140>(v));
+  v = dmax(v, dpp<0x141>(v));
+  v = dmax(v, dpp<0x4E>(v));
+  v = dmax(v, dpp<0xB1>(v));
+  return v;
+}
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int mask = 32; mask >= 1; mask >>= 1) v = dmax(v, __shfl_xor(v, mask));
+  v = g16_max(v);
+  v = dmax(v, __shfl_xor(v, 16));
+  v = dmax(v, __shfl_xor(v, 32));
   return v;
 }
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int mask = 32; mask >= 1; mask >>= 1) v += __shfl_xor(v, mask);
+  v = g16_sum(v);
+  v = v + __shfl_xor(v, 16);
+  v = v + __shfl_xor(v, 32);
   return v;
 }
 
+// Workgroup all-reduce of K values (every thread returns the same K results).  `slot` alternates
+// between calls so a buffer is never rewritten before every thread has read it (the barrier of
+// the following call orders the reads of the previous one).
+template <int N, int K, bool MAX>
+__device__ __forceinline__ void wg_reduce(Smem<N>& sm, double (&v)[K], int& slot) {
+  using Dm = Dim<N>;
+  static_assert(K <= 16, "");
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = MAX ? wave_max(v[k]) : wave_sum(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) sm.red[slot][wave][k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double r = sm.red[slot][0][k];
+    for (int w = 1; w < Dm::NW; ++w) r = MAX ? dmax(r, sm.red[slot][w][k]) : r + sm.red[slot][w][k];
+    v[k] = r;
+  }
+  slot ^= 1;
+}
+
 // ---- condensation: ConvexMpc.cpp:110-245 ----------------------------------------------------
-// Writes the dense Hessian (both triangles) to Pout[ld] and leaves the gradient in sm.qt and
-// the unscaled bounds in sm.lo / sm.hi.
+// Writes the dense Hessian (both triangles) to Pout[ld], the gradient to sm.qt and the unscaled
+// bounds to sm.lo / sm.hi.
 template <int N, int NT>
-__device__ void condense(Smem<N>& sm, const mpcqp_params& p, double* __restrict__ Pout, int ld) {
+__device__ __forceinline__ void condense(Smem<N>& sm, const mpcqp_params& p, double* __restrict__ Pout, int ld) {
   using Dm = Dim<N>;
   const int t = threadIdx.x;
   auto& C = sm.u.c;
   const double* rec = sm.rec;
   const double dt = rec[MPCQP_REC_DT];
   // calculate_A_mat_c (:110-130) + A_d = I + A_c dt (:150); S_{N-1} = Q
-  if (t < SD * SD) {
-    const int i = t / SD, j = t % SD;
+  for (int e = t; e < SD * SD; e += NT) {
+    const int i = e / SD, j = e % SD;
     const double yaw = rec[MPCQP_REC_EULER + 2];
     const double cy = cos(yaw), sy = sin(yaw);
     double ac = 0.0;
@@ -156,8 +184,8 @@ __device__ void condense(Smem<N>& sm, const mpcqp_params& p, double* __restrict_
     if (i == 2 && j == 8) ac = 1.0;
     if (i >= 3 && i <= 5 && j == i + 6) ac = 1.0;
     if (i == 11 && j == ND) ac = 1.0;
-    C.Ad[t] = (i == j ? 1.0 : 0.0) + ac * dt;
-    C.S[N - 1][t] = (i == j) ? 2 * p.q_weights[i] : 0.0;
+    C.Ad[e] = (i == j ? 1.0 : 0.0) + ac * dt;
+    C.S[N - 1][e] = (i == j) ? 2 * p.q_weights[i] : 0.0;
   }
   if (t == NT - 1) {
     // I_w = R I_b R' and its inverse (Eigen cofactor form), calculate_B_mat_c (:132-138)
@@ -188,18 +216,18 @@ __device__ void condense(Smem<N>& sm, const mpcqp_params& p, double* __restrict_
   __syncthreads();
   // S_k = Q + A_d' S_{k+1} A_d  (S_k = sum_{i>=k} (A^{i-k})' Q A^{i-k})
   for (int k = N - 2; k >= 0; --k) {
-    if (t < SD * SD) {
-      const int i = t / SD, j = t % SD;
+    for (int e = t; e < SD * SD; e += NT) {
+      const int i = e / SD, j = e % SD;
       double s = 0.0;
       for (int u = 0; u < SD; ++u) s += C.S[k + 1][i * SD + u] * C.Ad[u * SD + j];
-      C.T[t] = s;
+      C.T[e] = s;
     }
     __syncthreads();
-    if (t < SD * SD) {
-      const int i = t / SD, j = t % SD;
+    for (int e = t; e < SD * SD; e += NT) {
+      const int i = e / SD, j = e % SD;
       double s = 0.0;
       for (int u = 0; u < SD; ++u) s += C.Ad[u * SD + i] * C.T[u * SD + j];
-      C.S[k][t] = (i == j ? 2 * p.q_weights[i] : 0.0) + s;
+      C.S[k][e] = (i == j ? 2 * p.q_weights[i] : 0.0) + s;
     }
     __syncthreads();
   }
@@ -255,11 +283,11 @@ __device__ void condense(Smem<N>& sm, const mpcqp_params& p, double* __restrict_
       C.w[t] = 2 * p.q_weights[t] * (anew - rec[MPCQP_REC_XREF + SD * k + t]);
     }
     __syncthreads();
-    if (t < BQ) {
-      const int s = t / ND, b = t % ND;
+    for (int e = t; e < BQ; e += NT) {
+      const int s = e / ND, b = e % ND;
       double acc = 0.0;
       for (int u = 0; u < SD; ++u) acc += C.S[k][s * SD + u] * C.Bq[k][u * ND + b];
-      C.G[t] = acc;
+      C.G[e] = acc;
     }
     if (t < ND * (k + 1)) {  // gradient: g_j += B_qp(k,j)' Q (A_qp x0 - x_ref)_k
       const int j = t / ND, a = t % ND;
@@ -291,8 +319,8 @@ __device__ void condense(Smem<N>& sm, const mpcqp_params& p, double* __restrict_
   __syncthreads();
   if (t < Dm::n) sm.qt[t] = g_acc;
   // bounds (:223-245): per leg, identical for every horizon step
-  if (t < Dm::m) {
-    const int leg = (t % CD) / 5, row = t % 5;
+  for (int r = t; r < Dm::m; r += NT) {
+    const int leg = (r % CD) / 5, row = r % 5;
     const double c = rec[MPCQP_REC_CONTACTS + leg] != 0.0 ? 1.0 : 0.0;
     double l, u;
     switch (row) {
@@ -302,187 +330,230 @@ __device__ void condense(Smem<N>& sm, const mpcqp_params& p, double* __restrict_
       case 3: l = -OSQP_INF; u = 0; break;
       default: l = rec[MPCQP_REC_FZMIN] * c; u = rec[MPCQP_REC_FZMAX] * c; break;
     }
-    sm.lo[t] = l;
-    sm.hi[t] = u;
+    sm.lo[r] = l;
+    sm.hi[r] = u;
   }
   __syncthreads();
 }
 
-// ---- register tile helpers -----------------------------------------------------------------
-template <int BR>
-__device__ __forceinline__ void load_tile(double (&M)[BR][BC], const double* __restrict__ P, int n,
-                                          int tr, int tc) {
+// ---- register tile: rows 3f..3f+2 (the foot's variables) x cols tc*BC .. tc*BC+BC-1 ----------
+template <int N>
+__device__ __forceinline__ void load_tile(double (&M)[3][Dim<N>::BC], const double* __restrict__ P, int f,
+                                          int tc) {
+  using Dm = Dim<N>;
 #pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    const int r = tr * BR + i;
+  for (int i = 0; i < 3; ++i) {
+    const int r = 3 * f + i;
 #pragma unroll
-    for (int j = 0; j < BC; ++j) {
-      const int c = tc * BC + j;
-      M[i][j] = (r < n && c < n) ? P[(size_t)r * NP + c] : 0.0;
+    for (int j = 0; j < Dm::BC; ++j) {
+      const int c = tc * Dm::BC + j;
+      M[i][j] = (c < Dm::n) ? P[(size_t)r * Dm::NP + c] : 0.0;
     }
   }
 }
-template <int BR>
-__device__ __forceinline__ void store_tile(const double (&M)[BR][BC], double* __restrict__ P, int n,
-                                           int tr, int tc) {
+template <int N>
+__device__ __forceinline__ void store_tile(const double (&M)[3][Dim<N>::BC], double* __restrict__ P, int f,
+                                           int tc) {
+  using Dm = Dim<N>;
 #pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    const int r = tr * BR + i;
+  for (int i = 0; i < 3; ++i) {
+    const int r = 3 * f + i;
 #pragma unroll
-    for (int j = 0; j < BC; ++j) {
-      const int c = tc * BC + j;
-      if (r < n && c < n) P[(size_t)r * NP + c] = M[i][j];
+    for (int j = 0; j < Dm::BC; ++j) {
+      const int c = tc * Dm::BC + j;
+      if (c < Dm::n) P[(size_t)r * Dm::NP + c] = M[i][j];
     }
   }
 }
 
-// K = P~ + sigma I + A~' rho A~ (padded diagonal = 1), then in-place Gauss-Jordan inverse.
-template <int N, int BR>
-__device__ void build_and_invert(double (&M)[BR][BC], Smem<N>& sm, double sigma, int tr, int tc) {
+// A~' diag(rho) A~ rows for variable lanes (role a = tc - 5 of group f), from the row data of the
+// same group (same wave: LDS ordering, no barrier).
+template <int N>
+__device__ __forceinline__ void compute_bd_row(Smem<N>& sm, int f, int a) {
+  const int r0 = 5 * f;
+  const double* am = sm.am + r0;
+  const double* az = sm.az + r0;
+  const double* rv = sm.rho_v + r0;
+  double b0, b1, b2;
+  if (a == 0) {  // fx: rows 0,1 (main), fz coupling via az
+    b0 = am[0] * rv[0] * am[0] + am[1] * rv[1] * am[1];
+    b1 = 0.0;
+    b2 = am[0] * rv[0] * az[0] + am[1] * rv[1] * az[1];
+  } else if (a == 1) {  // fy: rows 2,3
+    b0 = 0.0;
+    b1 = am[2] * rv[2] * am[2] + am[3] * rv[3] * am[3];
+    b2 = am[2] * rv[2] * az[2] + am[3] * rv[3] * az[3];
+  } else {  // fz: az of rows 0-3 and the main coefficient of row 4
+    b0 = am[0] * rv[0] * az[0] + am[1] * rv[1] * az[1];
+    b1 = am[2] * rv[2] * az[2] + am[3] * rv[3] * az[3];
+    b2 = az[0] * rv[0] * az[0] + az[1] * rv[1] * az[1] + az[2] * rv[2] * az[2] + az[3] * rv[3] * az[3] +
+         am[4] * rv[4] * am[4];
+  }
+  const int c = 3 * f + a;
+  sm.BD[c][0] = b0;
+  sm.BD[c][1] = b1;
+  sm.BD[c][2] = b2;
+}
+
+// set_rho_vec (auxil.c) for the row lane (row r); on reclassify also decides the constraint type.
+template <int N>
+__device__ __forceinline__ void set_row_rho(Smem<N>& sm, int r, double rho, bool reclassify) {
+  int ct;
+  if (reclassify) {
+    if (sm.lo[r] < -OSQP_INF * MIN_SCALING && sm.hi[r] > OSQP_INF * MIN_SCALING)
+      ct = -1;
+    else if (sm.hi[r] - sm.lo[r] < RHO_TOL)
+      ct = 1;
+    else
+      ct = 0;
+    sm.ctype[r] = ct;
+  } else {
+    ct = sm.ctype[r];
+  }
+  double rr;
+  if (ct == -1)
+    rr = reclassify ? RHO_MIN : sm.rho_v[r];
+  else if (ct == 1)
+    rr = RHO_EQ_OVER_RHO_INEQ * rho;
+  else
+    rr = rho;
+  sm.rho_v[r] = rr;
+  sm.rho_inv[r] = 1. / rr;
+}
+
+// K = P~ + sigma I + A~' rho A~ from the tile already holding P~, then its inverse by block
+// Gauss-Jordan with 3x3 pivot blocks (pivot block kf = foot kf's diagonal block):
+//   A_kk <- P^-1,  A_kj <- P^-1 A_kj,  A_ik <- -A_ik P^-1,  A_ij <- A_ij - A_ik P^-1 A_kj.
+template <int N>
+__device__ __forceinline__ void build_and_invert(double (&M)[3][Dim<N>::BC], Smem<N>& sm, double sigma) {
   using Dm = Dim<N>;
-  constexpr int n = Dm::n;
+  constexpr int BC = Dm::BC, n = Dm::n;
+  const int t = opaque(threadIdx.x);
+  const int f = t >> 4, tc = t & 15;
 #pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    const int r = tr * BR + i;
+  for (int i = 0; i < 3; ++i) {
+    const int r = 3 * f + i;
 #pragma unroll
     for (int j = 0; j < BC; ++j) {
       const int c = tc * BC + j;
-      if (r < n && c < n) {
+      if (c < n) {
         double v = M[i][j];
         if (r == c) v += sigma;
-        if (r / 3 == c / 3) v += sm.BD[r / 3][(r % 3) * 3 + (c % 3)];
+        if (c / 3 == f) v += sm.BD[r][c - 3 * f];
         M[i][j] = v;
-      } else {
-        M[i][j] = (r == c) ? 1.0 : 0.0;
       }
     }
   }
-  // Gauss-Jordan: pivot k = kb*BC + ki (ki unrolled so every register index is static)
-  constexpr int KB = (n + BC - 1) / BC;
-  for (int kb = 0; kb < KB; ++kb) {
+  for (int kf = 0; kf < Dm::nf; ++kf) {
+    const int b = kf & 1;
+    // ---- phase A: the pivot group publishes P^-1 A_k. and the raw pivot columns ----
+    if (f == kf) {
+      // pivot block P = M[0..2][3kf..3kf+2] lives in 1-2 lanes of this group: publish via LDS
 #pragma unroll
-    for (int ki = 0; ki < BC; ++ki) {
-      const int k = kb * BC + ki;
-      if (k < n) {
-        double* rowb = sm.gj[k & 1][0];
-        double* colb = sm.gj[k & 1][1];
-        const bool own_row = tr == kb * (BC / BR) + ki / BR;
-        const bool own_col = tc == kb;
+      for (int j = 0; j < BC; ++j) {
+        const int c = tc * BC + j;
+        if (c >= 3 * kf && c < 3 * kf + 3)
+#pragma unroll
+          for (int i = 0; i < 3; ++i) sm.u.g.p[b][i * 3 + (c - 3 * kf)] = M[i][j];
+      }
+      double P[9];
+#pragma unroll
+      for (int e = 0; e < 9; ++e) P[e] = sm.u.g.p[b][e];  // same wave: ordered after the stores
+      auto cof = [&](int i, int j) {
+        const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+        return P[i1 * 3 + j1] * P[i2 * 3 + j2] - P[i1 * 3 + j2] * P[i2 * 3 + j1];
+      };
+      const double det = (cof(0, 0) * P[0] + cof(1, 0) * P[3]) + cof(2, 0) * P[6];
+      const double invdet = 1.0 / det;
+      double Pi[9];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Pi[j * 3 + i] = cof(i, j) * invdet;
+#pragma unroll
+      for (int j = 0; j < BC; ++j) {
+        const double r0 = M[0][j], r1 = M[1][j], r2 = M[2][j];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) sm.u.g.r[b][i][tc * BC + j] = (Pi[i * 3] * r0 + Pi[i * 3 + 1] * r1) + Pi[i * 3 + 2] * r2;
+      }
+      if (tc == 0) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) sm.u.g.p[b][e] = Pi[e];
+      }
+    }
+    // pivot columns: every group's lanes holding cols 3kf..3kf+2 publish their 3 rows
+#pragma unroll
+    for (int j = 0; j < BC; ++j) {
+      const int c = tc * BC + j;
+      if (c >= 3 * kf && c < 3 * kf + 3)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) sm.u.g.c[b][3 * f + i][c - 3 * kf] = M[i][j];
+    }
+    __syncthreads();
+    // ---- phase B: rank-3 update of every tile, then the pivot row/column fix-ups ----
+    double Ck[3][3], Pi[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) Ck[i][q] = sm.u.g.c[b][3 * f + i][q];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) Pi[e] = sm.u.g.p[b][e];
+    const bool own_row = f == kf;
+#pragma unroll
+    for (int j = 0; j < BC; ++j) {
+      const int c = tc * BC + j;
+      const double R0 = sm.u.g.r[b][0][c], R1 = sm.u.g.r[b][1][c], R2 = sm.u.g.r[b][2][c];
+      const bool kcol = c >= 3 * kf && c < 3 * kf + 3;
+      const int q = c - 3 * kf;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        double v;
+        // column q of P^-1 selected without a runtime register index
+        const double p0 = q == 0 ? Pi[0] : q == 1 ? Pi[1] : Pi[2];
+        const double p1 = q == 0 ? Pi[3] : q == 1 ? Pi[4] : Pi[5];
+        const double p2 = q == 0 ? Pi[6] : q == 1 ? Pi[7] : Pi[8];
         if (own_row) {
-#pragma unroll
-          for (int j = 0; j < BC; ++j) rowb[tc * BC + j] = M[ki % BR][j];
+          v = kcol ? (i == 0 ? p0 : i == 1 ? p1 : p2) : (i == 0 ? R0 : i == 1 ? R1 : R2);
+        } else if (kcol) {
+          v = -((Ck[i][0] * p0 + Ck[i][1] * p1) + Ck[i][2] * p2);
+        } else {
+          v = M[i][j] - ((Ck[i][0] * R0 + Ck[i][1] * R1) + Ck[i][2] * R2);
         }
-        if (own_col) {
-#pragma unroll
-          for (int i = 0; i < BR; ++i) colb[tr * BR + i] = M[i][ki];
-        }
-        __syncthreads();
-        const double inv = 1.0 / rowb[k];
-        double rk[BC], ck[BR];
-#pragma unroll
-        for (int j = 0; j < BC; ++j) rk[j] = rowb[tc * BC + j] * inv;
-#pragma unroll
-        for (int i = 0; i < BR; ++i) ck[i] = colb[tr * BR + i];
-#pragma unroll
-        for (int i = 0; i < BR; ++i)
-#pragma unroll
-          for (int j = 0; j < BC; ++j) M[i][j] = fma(-ck[i], rk[j], M[i][j]);
-        if (own_row) {
-#pragma unroll
-          for (int j = 0; j < BC; ++j) M[ki % BR][j] = rk[j];
-        }
-        if (own_col) {
-#pragma unroll
-          for (int i = 0; i < BR; ++i) M[i][ki] = -ck[i] * inv;
-        }
-        if (own_row && own_col) M[ki % BR][ki] = inv;
+        M[i][j] = v;
       }
     }
   }
   __syncthreads();
-}
-
-// set_rho_vec (auxil.c) + A~' rho A~ blocks
-template <int N>
-__device__ void set_rho_and_blocks(Smem<N>& sm, double rho, bool reclassify) {
-  using Dm = Dim<N>;
-  const int t = threadIdx.x;
-  if (t < Dm::nf) {
-    const int f = t;
-    double rv[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const int r = 5 * f + k;
-      int ct;
-      if (reclassify) {
-        if (sm.lo[r] < -OSQP_INF * MIN_SCALING && sm.hi[r] > OSQP_INF * MIN_SCALING)
-          ct = -1;
-        else if (sm.hi[r] - sm.lo[r] < RHO_TOL)
-          ct = 1;
-        else
-          ct = 0;
-        sm.ctype[r] = ct;
-      } else {
-        ct = sm.ctype[r];
-      }
-      double rr;
-      if (ct == -1) {
-        rr = reclassify ? RHO_MIN : sm.rho_v[r];
-      } else if (ct == 1) {
-        rr = RHO_EQ_OVER_RHO_INEQ * rho;
-      } else {
-        rr = rho;
-      }
-      sm.rho_v[r] = rr;
-      sm.rho_inv[r] = 1. / rr;
-      rv[k] = rr;
-    }
-    const double* a = sm.A9[f];
-    double* bd = sm.BD[f];
-    // rows: 0:(x,z) 1:(x,z) 2:(y,z) 3:(y,z) 4:(z)
-    bd[0] = a[0] * rv[0] * a[0] + a[2] * rv[1] * a[2];
-    bd[1] = 0.0;
-    bd[2] = a[0] * rv[0] * a[1] + a[2] * rv[1] * a[3];
-    bd[3] = 0.0;
-    bd[4] = a[4] * rv[2] * a[4] + a[6] * rv[3] * a[6];
-    bd[5] = a[4] * rv[2] * a[5] + a[6] * rv[3] * a[7];
-    bd[6] = bd[2];
-    bd[7] = bd[5];
-    bd[8] = a[1] * rv[0] * a[1] + a[3] * rv[1] * a[3] + a[5] * rv[2] * a[5] + a[7] * rv[3] * a[7] +
-            a[8] * rv[4] * a[8];
-  }
 }
 
 // ---- the solver kernel ---------------------------------------------------------------------
-template <int N, int BR>
-__global__ __launch_bounds__((NP / BR) * 16) void solve_kernel(
+template <int N>
+__global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
     const double* __restrict__ recs, int batch, mpcqp_result* __restrict__ results,
-    double* __restrict__ solution, double* __restrict__ work,
-    double* __restrict__ trace, int trace_cap, mpcqp_params p) {
+    double* __restrict__ solution, double* __restrict__ work, double* __restrict__ trace, int trace_cap,
+    mpcqp_params p) {
   using Dm = Dim<N>;
-  constexpr int NT = (NP / BR) * 16;
-  constexpr int n = Dm::n, m = Dm::m, nf = Dm::nf;
-  static_assert(nf <= 64, "feet must fit in wave 0");
+  constexpr int NT = Dm::NT, BC = Dm::BC, n = Dm::n, m = Dm::m, nf = Dm::nf;
   __shared__ Smem<N> sm;
-  const int t = threadIdx.x;
-  const int tr = t >> 4, tc = t & 15;
-  const int lane = t & 63;
-  const bool wave0 = t < 64;
   const int inst = blockIdx.x;
   if (inst >= batch) return;
-  double* __restrict__ Pw = work + (size_t)inst * NP * NP;
+  const int t0 = threadIdx.x;
+  double* __restrict__ Pw = work + (size_t)inst * n * Dm::NP;
   const double alpha = p.alpha, sigma = p.sigma;
-  double M[BR][BC];
+  double M[3][BC];
+  int rslot = 0;
+
+  // ---- 0. record -> LDS, non-finite guard --------------------------------------------------
   {
     const double* rec_g = recs + (size_t)inst * Dm::rec;
     bool bad = false;
-    for (int e = t; e < Dm::rec; e += NT) {
+    for (int e = t0; e < Dm::rec; e += NT) {
       const double v = rec_g[e];
       sm.rec[e] = v;
       bad |= !isfinite(v);
     }
     if (__syncthreads_or(bad)) {
-      if (t == 0) {
+      if (t0 == 0) {
         mpcqp_result r;
         for (int k = 0; k < ND; ++k) { r.u0[k] = NAN; r.f_body[k] = 0.0; }
         r.obj_val = NAN; r.pri_res = NAN; r.dua_res = NAN; r.rho = p.rho;
@@ -490,515 +561,427 @@ __global__ __launch_bounds__((NP / BR) * 16) void solve_kernel(
         results[inst] = r;
       }
       if (solution)
-        for (int e = t; e < n; e += NT) solution[(size_t)inst * n + e] = NAN;
+        for (int e = t0; e < n; e += NT) solution[(size_t)inst * n + e] = NAN;
       return;
     }
+  }
 
-    if (t == 0) sm.ctl[2] = 0;
-    // ---- 1. condensation -> workspace (unscaled H), sm.qt (gradient), sm.lo/hi --------------
-    condense<N, NT>(sm, p, Pw, NP);
+  // ---- 1. condensation -> workspace (unscaled H), sm.qt (gradient), sm.lo/hi ----------------
+  condense<N, NT>(sm, p, Pw, Dm::NP);
 
-    // ---- 2. OSQP scale_data (Ruiz), P in registers ------------------------------------------
-    load_tile<BR>(M, Pw, n, tr, tc);
-    if (t < n) { sm.D[t] = 1.0; }
-    if (t < m) { sm.E[t] = 1.0; }
-    if (t < nf) {
-      const double mu = sm.rec[MPCQP_REC_MU];
-      double* a = sm.A9[t];
-      a[0] = 1; a[1] = mu; a[2] = 1; a[3] = -mu; a[4] = 1; a[5] = mu; a[6] = 1; a[7] = -mu; a[8] = 1;
-    }
-    if (t == 0) sm.cst[0] = 1.0;
-    __syncthreads();
-    auto& RS = sm.u.r;
-    for (int pass = 0; pass < p.scaling; ++pass) {
-      // colnorm(P) = rownorm (P symmetric, both triangles stored identically)
-      {
-        double pm[BR];
-#pragma unroll
-        for (int i = 0; i < BR; ++i) {
-          double mx = 0.0;
-#pragma unroll
-          for (int j = 0; j < BC; ++j) mx = dmax(mx, dabs(M[i][j]));
-          pm[i] = mx;
-        }
-        const double r = rs16<BR, true>(pm, tc);
-        if ((tc & ((16 / BR) - 1)) == 0) RS.colP[tr * BR + (tc >> (4 - (BR == 1 ? 0 : BR == 2 ? 1 : BR == 4 ? 2 : 3)))] = r;
-      }
-      __syncthreads();
-      if (t < n) {  // D_temp (compute_inf_norm_cols_KKT + limit + sqrt + recip)
-        const int f = t / 3, a = t % 3;
-        const double* A9 = sm.A9[f];
-        double ca;
-        if (a == 0) ca = dmax(dabs(A9[0]), dabs(A9[2]));
-        else if (a == 1) ca = dmax(dabs(A9[4]), dabs(A9[6]));
-        else ca = dmax(dmax(dmax(dmax(dabs(A9[1]), dabs(A9[3])), dabs(A9[5])), dabs(A9[7])), dabs(A9[8]));
-        double d = dmax(RS.colP[t], ca);
-        d = limit_scaling(d);
-        RS.Dt[t] = 1.0 / sqrt(d);
-      }
-      if (t < m) {
-        const int f = t / 5, k = t % 5;
-        const double* A9 = sm.A9[f];
-        double e = (k < 4) ? dmax(dabs(A9[2 * k]), dabs(A9[2 * k + 1])) : dabs(A9[8]);
-        e = limit_scaling(e);
-        RS.Et[t] = 1.0 / sqrt(e);
-      }
-      __syncthreads();
-      // P <- D P D (premult by row of the upper-triangle entry, then postmult by its column)
-#pragma unroll
-      for (int i = 0; i < BR; ++i) {
-        const int r = tr * BR + i;
-#pragma unroll
-        for (int j = 0; j < BC; ++j) {
-          const int c = tc * BC + j;
-          if (r < n && c < n) {
-            const int pr = r < c ? r : c, pc = r < c ? c : r;
-            M[i][j] = (M[i][j] * RS.Dt[pr]) * RS.Dt[pc];
-          }
-        }
-      }
-      if (t < m) {  // A <- E A D
-        const int f = t / 5, k = t % 5;
-        double* A9 = sm.A9[f];
-        const double et = RS.Et[t];
-        if (k < 4) {
-          const int mainc = 3 * f + (k < 2 ? 0 : 1);
-          A9[2 * k] = (A9[2 * k] * et) * RS.Dt[mainc];
-          A9[2 * k + 1] = (A9[2 * k + 1] * et) * RS.Dt[3 * f + 2];
-        } else {
-          A9[8] = (A9[8] * et) * RS.Dt[3 * f + 2];
-        }
-        sm.E[t] *= et;
-      }
-      if (t < n) {
-        sm.qt[t] = RS.Dt[t] * sm.qt[t];
-        sm.D[t] = sm.D[t] * RS.Dt[t];
-      }
-      __syncthreads();
-      // cost normalization
-      {
-        double pm[BR];
-#pragma unroll
-        for (int i = 0; i < BR; ++i) {
-          double mx = 0.0;
-#pragma unroll
-          for (int j = 0; j < BC; ++j) mx = dmax(mx, dabs(M[i][j]));
-          pm[i] = mx;
-        }
-        const double r = rs16<BR, true>(pm, tc);
-        if ((tc & ((16 / BR) - 1)) == 0) RS.colP[tr * BR + (tc >> (4 - (BR == 1 ? 0 : BR == 2 ? 1 : BR == 4 ? 2 : 3)))] = r;
-      }
-      __syncthreads();
-      if (wave0) {
-        double s = 0.0, qn = 0.0;
-        for (int c = lane; c < n; c += 64) {
-          s += RS.colP[c];
-          qn = dmax(qn, dabs(sm.qt[c]));
-        }
-        s = wave_sum(s);
-        qn = wave_max(qn);
-        double c_temp = s / n;
-        qn = limit_scaling(qn);
-        c_temp = dmax(c_temp, qn);
-        c_temp = limit_scaling(c_temp);
-        c_temp = 1. / c_temp;
-        if (lane == 0) {
-          sm.cst[3] = c_temp;
-          sm.cst[0] *= c_temp;
-        }
-      }
-      __syncthreads();
-      const double c_temp = sm.cst[3];
-#pragma unroll
-      for (int i = 0; i < BR; ++i)
-#pragma unroll
-        for (int j = 0; j < BC; ++j) M[i][j] *= c_temp;
-      if (t < n) sm.qt[t] *= c_temp;
-      __syncthreads();
-    }
-    // cinv, Dinv, Einv, scaled bounds
-    if (t == 0) sm.cst[1] = 1. / sm.cst[0];
-    if (t < n) sm.Dinv[t] = 1. / sm.D[t];
-    if (t < m) {
-      sm.Einv[t] = 1. / sm.E[t];
-      sm.lo[t] = sm.E[t] * sm.lo[t];
-      sm.hi[t] = sm.E[t] * sm.hi[t];
-    }
-    __syncthreads();
-    store_tile<BR>(M, Pw, n, tr, tc);  // scaled P~ kept for rho refactorizations
-    double rho = dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
-    set_rho_and_blocks<N>(sm, rho, true);
-    // zero iterates (cold start) and padded mat-vec lanes
-    for (int e = t; e < NP; e += NT) { sm.rhs[e] = 0.0; sm.xt[e] = 0.0; }
-    if (t < n) { sm.X[t] = 0.0; sm.PX[t] = 0.0; }
-    if (t < m) { sm.Z[t] = 0.0; sm.Y[t] = 0.0; }
-    __syncthreads();
-    build_and_invert<N, BR>(M, sm, sigma, tr, tc);
+  const int f = t0 >> 4, tc = t0 & 15;
+  const bool row_lane = tc < 5, var_lane = tc >= 5 && tc < 8;
+  const int r = 5 * f + tc;        // constraint row of a row lane
+  const int a = tc - 5;            // variable role of a var lane
+  const int c = 3 * f + (a < 0 ? 0 : a);  // variable of a var lane
 
-    // ---- 3. ADMM ------------------------------------------------------------------------------
-    const double cinv = sm.cst[1], cc = sm.cst[0];
-    int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0;
-    double pri_res = 0.0, dua_res = 0.0;
-    int ntrace = 0;
-    for (int iter = 1; iter <= p.max_iter; ++iter) {
-      const int t = opaque(threadIdx.x);
-      const int tr = t >> 4, tc = t & 15;
-      const int lane = t & 63;
-      // (a) rhs = sigma x - q~ + A~'(rho z - y)   [compute_rhs + reduced KKT right-hand side]
-      if (t < nf) {
-        const int f = t;
-        const double* a = sm.A9[f];
-        double tt[5];
+  // ---- 2. OSQP scale_data (Ruiz), P in registers ---------------------------------------------
+  load_tile<N>(M, Pw, f, tc);
+  if (row_lane) {  // unscaled friction pyramid row (ConvexMpc.cpp:46-58)
+    const double mu = sm.rec[MPCQP_REC_MU];
+    sm.am[r] = 1.0;
+    sm.az[r] = tc == 4 ? 0.0 : ((tc & 1) ? -mu : mu);
+    sm.E[r] = 1.0;
+  }
+  if (var_lane) sm.D[c] = 1.0;
+  double cost_c = 1.0;
+  for (int pass = 0; pass < p.scaling; ++pass) {
+    // D_temp: column inf-norm of [P; A] per variable (P symmetric: row norms of the tiles)
+    double pm[3];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) tt[k] = sm.rho_v[5 * f + k] * sm.Z[5 * f + k] - sm.Y[5 * f + k];
-        const double bx = (sigma * sm.X[3 * f + 0] - sm.qt[3 * f + 0]);
-        const double by = (sigma * sm.X[3 * f + 1] - sm.qt[3 * f + 1]);
-        const double bz = (sigma * sm.X[3 * f + 2] - sm.qt[3 * f + 2]);
-        sm.rhs[3 * f + 0] = (bx + a[0] * tt[0]) + a[2] * tt[1];
-        sm.rhs[3 * f + 1] = (by + a[4] * tt[2]) + a[6] * tt[3];
-        sm.rhs[3 * f + 2] = ((((bz + a[1] * tt[0]) + a[3] * tt[1]) + a[5] * tt[2]) + a[7] * tt[3]) + a[8] * tt[4];
-      }
-      __syncthreads();
-      // (b) x~ = K^-1 rhs
-      {
-        double v[BC];
+    for (int i = 0; i < 3; ++i) {
+      double mx = 0.0;
 #pragma unroll
-        for (int j = 0; j < BC; ++j) v[j] = sm.rhs[tc * BC + j];
-        double s[BR];
+      for (int j = 0; j < BC; ++j) mx = dmax(mx, dabs(M[i][j]));
+      pm[i] = g16_max(mx);
+    }
+    if (var_lane) {
+      const int r0 = 5 * f;
+      double ca;
+      if (a == 0) ca = dmax(dabs(sm.am[r0]), dabs(sm.am[r0 + 1]));
+      else if (a == 1) ca = dmax(dabs(sm.am[r0 + 2]), dabs(sm.am[r0 + 3]));
+      else ca = dmax(dmax(dmax(dmax(dabs(sm.az[r0]), dabs(sm.az[r0 + 1])), dabs(sm.az[r0 + 2])), dabs(sm.az[r0 + 3])),
+                     dabs(sm.am[r0 + 4]));
+      const double pc = a == 0 ? pm[0] : a == 1 ? pm[1] : pm[2];
+      sm.Dt[c] = 1.0 / sqrt(limit_scaling(dmax(pc, ca)));
+    }
+    double et = 1.0;
+    if (row_lane) et = 1.0 / sqrt(limit_scaling(tc == 4 ? dabs(sm.am[r]) : dmax(dabs(sm.am[r]), dabs(sm.az[r]))));
+    __syncthreads();
+    // P <- D P D (premultiply by the row of the upper-triangle entry, then its column)
+    double drow[3];
 #pragma unroll
-        for (int i = 0; i < BR; ++i) {
-          double acc = 0.0;
+    for (int i = 0; i < 3; ++i) drow[i] = sm.Dt[3 * f + i];
 #pragma unroll
-          for (int j = 0; j < BC; ++j) acc = fma(M[i][j], v[j], acc);
-          s[i] = acc;
-        }
-        const double r = rs16<BR, false>(s, tc);
-        if ((tc & ((16 / BR) - 1)) == 0) sm.xt[tr * BR + (tc >> (4 - (BR == 1 ? 0 : BR == 2 ? 1 : BR == 4 ? 2 : 3)))] = r;
-      }
-      __syncthreads();
-      // (c) x, z, y updates per foot (update_x, update_z + project, update_y)
-      const bool is_check = p.check_termination && (iter % p.check_termination == 0);
-      const bool is_adapt = p.adaptive_rho && p.adaptive_rho_interval && (iter % p.adaptive_rho_interval == 0);
-      const bool last = iter == p.max_iter;
-      const bool need_info = is_check || is_adapt || last;
-      double part[14];
+    for (int j = 0; j < BC; ++j) {
+      const int cc = tc * BC + j;
+      if (cc < n) {
+        const double dc = sm.Dt[cc];
 #pragma unroll
-      for (int k = 0; k < 14; ++k) part[k] = 0.0;
-      double dxv[3] = {0, 0, 0}, dyv[5] = {0, 0, 0, 0, 0}, pxo[3] = {0, 0, 0}, pxn[3] = {0, 0, 0};
-      if (t < nf) {
-        const int f = t;
-        const double* a = sm.A9[f];
-        const double xt0 = sm.xt[3 * f], xt1 = sm.xt[3 * f + 1], xt2 = sm.xt[3 * f + 2];
-        double zt[5];
-        zt[0] = a[0] * xt0 + a[1] * xt2;
-        zt[1] = a[2] * xt0 + a[3] * xt2;
-        zt[2] = a[4] * xt1 + a[5] * xt2;
-        zt[3] = a[6] * xt1 + a[7] * xt2;
-        zt[4] = a[8] * xt2;
-        const double xtv[3] = {xt0, xt1, xt2};
-        const double* bd = sm.BD[f];
-        double xn[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const double xo = sm.X[3 * f + k];
-          xn[k] = alpha * xtv[k] + (1.0 - alpha) * xo;
-          dxv[k] = xn[k] - xo;
-          // P~ x~ from the KKT identity: (P~ + sigma I + A~'rho A~) x~ = rhs
-          const double pxt = sm.rhs[3 * f + k] - sigma * xtv[k] -
-                             ((bd[3 * k] * xt0 + bd[3 * k + 1] * xt1) + bd[3 * k + 2] * xt2);
-          pxo[k] = sm.PX[3 * f + k];
-          pxn[k] = alpha * pxt + (1.0 - alpha) * pxo[k];
-          sm.X[3 * f + k] = xn[k];
-          sm.PX[3 * f + k] = pxn[k];
-        }
-        double zn[5], yn[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const int r = 5 * f + k;
-          const double zo = sm.Z[r], yo = sm.Y[r];
-          const double zr = alpha * zt[k] + (1.0 - alpha) * zo;
-          zn[k] = dmin(dmax(zr + sm.rho_inv[r] * yo, sm.lo[r]), sm.hi[r]);
-          dyv[k] = sm.rho_v[r] * (zr - zn[k]);
-          yn[k] = yo + dyv[k];
-          sm.Z[r] = zn[k];
-          sm.Y[r] = yn[k];
-        }
-        if (need_info) {
-          double ax[5];
-          ax[0] = a[0] * xn[0] + a[1] * xn[2];
-          ax[1] = a[2] * xn[0] + a[3] * xn[2];
-          ax[2] = a[4] * xn[1] + a[5] * xn[2];
-          ax[3] = a[6] * xn[1] + a[7] * xn[2];
-          ax[4] = a[8] * xn[2];
-#pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            const int r = 5 * f + k;
-            const double pr = ax[k] + (-1.0) * zn[k];
-            const double ei = sm.Einv[r];
-            part[0] = dmax(part[0], dabs(ei * pr));
-            part[1] = dmax(part[1], dabs(pr));
-            part[2] = dmax(part[2], dabs(ei * zn[k]));
-            part[3] = dmax(part[3], dabs(zn[k]));
-            part[4] = dmax(part[4], dabs(ei * ax[k]));
-            part[5] = dmax(part[5], dabs(ax[k]));
-          }
-          double aty[3];
-          aty[0] = a[0] * yn[0] + a[2] * yn[1];
-          aty[1] = a[4] * yn[2] + a[6] * yn[3];
-          aty[2] = (((a[1] * yn[0] + a[3] * yn[1]) + a[5] * yn[2]) + a[7] * yn[3]) + a[8] * yn[4];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            const int c = 3 * f + k;
-            const double di = sm.Dinv[c], q = sm.qt[c];
-            const double d = (q + 1.0 * pxn[k]) + 1.0 * aty[k];
-            part[6] = dmax(part[6], dabs(di * d));
-            part[7] = dmax(part[7], dabs(d));
-            part[8] = dmax(part[8], dabs(di * q));
-            part[9] = dmax(part[9], dabs(q));
-            part[10] = dmax(part[10], dabs(di * aty[k]));
-            part[11] = dmax(part[11], dabs(aty[k]));
-            part[12] = dmax(part[12], dabs(di * pxn[k]));
-            part[13] = dmax(part[13], dabs(pxn[k]));
-          }
-        }
-      }
-      if (need_info) {
-        if (wave0) {
-          double mx[14];
-#pragma unroll
-          for (int k = 0; k < 14; ++k) mx[k] = wave_max(part[k]);
-          pri_res = mx[0];
-          dua_res = cinv * mx[6];
-          iters = iter;
-          int st = MPCQP_STATUS_UNSOLVED;
-          bool done = false;
-          // check_termination (approximate = 0, then 1 at max_iter)
-          for (int approx = 0; approx < 2 && !done; ++approx) {
-            if (approx == 1 && !last) break;
-            if (!is_check && !last) break;
-            double eps_abs = p.eps_abs, eps_rel = p.eps_rel, eps_pinf = p.eps_prim_inf, eps_dinf = p.eps_dual_inf;
-            if (pri_res > OSQP_INF || dua_res > OSQP_INF) {
-              st = MPCQP_STATUS_NON_CVX;
-              done = true;
-              break;
-            }
-            if (approx) { eps_abs *= 10; eps_rel *= 10; eps_pinf *= 10; eps_dinf *= 10; }
-            const double eps_prim = eps_abs + eps_rel * dmax(mx[2], mx[4]);
-            const bool prim_ok = pri_res < eps_prim;
-            bool prim_inf = false, dual_inf = false;
-            if (!prim_ok) {
-              // is_primal_infeasible: project delta_y onto the polar of the recession cone
-              double ndy = 0.0, lhs = 0.0;
-              double dyp[5];
-#pragma unroll
-              for (int k = 0; k < 5; ++k) {
-                dyp[k] = dyv[k];
-                if (t < nf) {
-                  const int r = 5 * t + k;
-                  if (sm.hi[r] > OSQP_INF * MIN_SCALING) {
-                    if (sm.lo[r] < -OSQP_INF * MIN_SCALING) dyp[k] = 0.0;
-                    else dyp[k] = dmin(dyp[k], 0.0);
-                  } else if (sm.lo[r] < -OSQP_INF * MIN_SCALING) {
-                    dyp[k] = dmax(dyp[k], 0.0);
-                  }
-                  dyv[k] = dyp[k];
-                  ndy = dmax(ndy, dabs(sm.E[r] * dyp[k]));
-                  lhs += sm.hi[r] * dmax(dyp[k], 0.0) + sm.lo[r] * dmin(dyp[k], 0.0);
-                } else {
-                  dyp[k] = 0.0;
-                }
-              }
-              ndy = wave_max(ndy);
-              if (ndy > DIV_TOL) {
-                lhs = wave_sum(lhs);
-                if (lhs < eps_pinf * ndy) {
-                  double atn = 0.0;
-                  if (t < nf) {
-                    const double* a = sm.A9[t];
-                    const double at0 = a[0] * dyp[0] + a[2] * dyp[1];
-                    const double at1 = a[4] * dyp[2] + a[6] * dyp[3];
-                    const double at2 = (((a[1] * dyp[0] + a[3] * dyp[1]) + a[5] * dyp[2]) + a[7] * dyp[3]) + a[8] * dyp[4];
-                    atn = dmax(dmax(dabs(sm.Dinv[3 * t] * at0), dabs(sm.Dinv[3 * t + 1] * at1)),
-                               dabs(sm.Dinv[3 * t + 2] * at2));
-                  }
-                  atn = wave_max(atn);
-                  prim_inf = atn < eps_pinf * ndy;
-                }
-              }
-            }
-            const double eps_dual = eps_abs + eps_rel * (cinv * dmax(dmax(mx[8], mx[10]), mx[12]));
-            const bool dual_ok = dua_res < eps_dual;
-            if (!dual_ok) {
-              // is_dual_infeasible
-              double ndx = 0.0, qdx = 0.0, npdx = 0.0;
-              if (t < nf) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                  const int c = 3 * t + k;
-                  ndx = dmax(ndx, dabs(sm.D[c] * dxv[k]));
-                  qdx += sm.qt[c] * dxv[k];
-                  npdx = dmax(npdx, dabs(sm.Dinv[c] * (pxn[k] - pxo[k])));
-                }
-              }
-              ndx = wave_max(ndx);
-              if (ndx > DIV_TOL) {
-                qdx = wave_sum(qdx);
-                if (qdx < cc * eps_dinf * ndx) {
-                  npdx = wave_max(npdx);
-                  if (npdx < cc * eps_dinf * ndx) {
-                    double viol = 0.0;
-                    if (t < nf) {
-                      const double* a = sm.A9[t];
-                      double adx[5];
-                      adx[0] = a[0] * dxv[0] + a[1] * dxv[2];
-                      adx[1] = a[2] * dxv[0] + a[3] * dxv[2];
-                      adx[2] = a[4] * dxv[1] + a[5] * dxv[2];
-                      adx[3] = a[6] * dxv[1] + a[7] * dxv[2];
-                      adx[4] = a[8] * dxv[2];
-#pragma unroll
-                      for (int k = 0; k < 5; ++k) {
-                        const int r = 5 * t + k;
-                        const double v = sm.Einv[r] * adx[k];
-                        if ((sm.hi[r] < OSQP_INF * MIN_SCALING && v > eps_dinf * ndx) ||
-                            (sm.lo[r] > -OSQP_INF * MIN_SCALING && v < -eps_dinf * ndx))
-                          viol = 1.0;
-                      }
-                    }
-                    viol = wave_max(viol);
-                    dual_inf = viol == 0.0;
-                  }
-                }
-              }
-            }
-            if (prim_ok && dual_ok) {
-              st = approx ? MPCQP_STATUS_SOLVED_INACCURATE : MPCQP_STATUS_SOLVED;
-              done = true;
-            } else if (prim_inf) {
-              st = approx ? MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE : MPCQP_STATUS_PRIMAL_INFEASIBLE;
-              done = true;
-            } else if (dual_inf) {
-              st = approx ? MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE : MPCQP_STATUS_DUAL_INFEASIBLE;
-              done = true;
-            }
-            if (!done && approx == 0 && is_adapt) {
-              // adapt_rho (runs before the post-loop approximate check in osqp_solve)
-              const double pr_n = mx[1] / (dmax(mx[3], mx[5]) + DIV_TOL);
-              const double du_n = mx[7] / (dmax(dmax(mx[9], mx[11]), mx[13]) + DIV_TOL);
-              double est = rho * sqrt(pr_n / (du_n + DIV_TOL));
-              est = dmin(dmax(est, RHO_MIN), RHO_MAX);
-              if (est > rho * p.adaptive_rho_tolerance || est < rho / p.adaptive_rho_tolerance) {
-                rho = dmin(dmax(est, RHO_MIN), RHO_MAX);
-                rho_updates += 1;
-                if (lane == 0) sm.ctl[2] = last ? 0 : 1;
-              }
-            }
-          }
-          if (!is_check && !last && is_adapt) {
-            // adapt-only iteration (adaptive_rho_interval not a multiple of check_termination)
-            const double pr_n = mx[1] / (dmax(mx[3], mx[5]) + DIV_TOL);
-            const double du_n = mx[7] / (dmax(dmax(mx[9], mx[11]), mx[13]) + DIV_TOL);
-            double est = rho * sqrt(pr_n / (du_n + DIV_TOL));
-            est = dmin(dmax(est, RHO_MIN), RHO_MAX);
-            if (est > rho * p.adaptive_rho_tolerance || est < rho / p.adaptive_rho_tolerance) {
-              rho = dmin(dmax(est, RHO_MIN), RHO_MAX);
-              rho_updates += 1;
-              if (lane == 0) sm.ctl[2] = 1;
-            }
-          }
-          if (last && !done) st = MPCQP_STATUS_MAX_ITER_REACHED;
-          if (last) done = true;
-          status = st;
-          if (lane == 0) {
-            sm.ctl[1] = done ? 1 : 0;
-            sm.ctl[3] = st;
-            sm.cst[2] = rho;
-            if (trace && inst < trace_cap && ntrace < MPCQP_TRACE_LEN && is_check) {
-              double* tp = trace + ((size_t)inst * MPCQP_TRACE_LEN + ntrace) * 4;
-              tp[0] = iter; tp[1] = pri_res; tp[2] = dua_res; tp[3] = rho;
-            }
-          }
-          ntrace += is_check ? 1 : 0;
-        }
-        __syncthreads();
-        const bool done = sm.ctl[1] != 0;
-        rho = sm.cst[2];
-        if (sm.ctl[2]) {
-          // osqp_update_rho: new rho_vec, refactor K (reload P~ from the workspace)
-          __syncthreads();
-          if (t == 0) sm.ctl[2] = 0;
-          set_rho_and_blocks<N>(sm, rho, false);
-          load_tile<BR>(M, Pw, n, tr, tc);
-          __syncthreads();
-          build_and_invert<N, BR>(M, sm, sigma, tr, tc);
-        }
-        if (done) {
-          status = sm.ctl[3];
-          break;
+        for (int i = 0; i < 3; ++i) {
+          const int rr = 3 * f + i;
+          M[i][j] = rr <= cc ? (M[i][j] * drow[i]) * dc : (M[i][j] * dc) * drow[i];
         }
       }
     }
-    if (t == 0) sm.ctl[2] = 0;
-    // ---- 4. store_solution + unscale + compute_grf extraction -----------------------------------
-    const bool has_sol = status != MPCQP_STATUS_PRIMAL_INFEASIBLE &&
-                         status != MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE &&
-                         status != MPCQP_STATUS_DUAL_INFEASIBLE &&
-                         status != MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE &&
-                         status != MPCQP_STATUS_NON_CVX;
-    if (wave0) {
-      double ob = 0.0;
-      if (t < nf) {
+    if (row_lane) {  // A <- E A D
+      const int mainv = 3 * f + (tc < 2 ? 0 : tc < 4 ? 1 : 2);
+      sm.am[r] = (sm.am[r] * et) * sm.Dt[mainv];
+      if (tc < 4) sm.az[r] = (sm.az[r] * et) * sm.Dt[3 * f + 2];
+      sm.E[r] *= et;
+    }
+    if (var_lane) {
+      sm.qt[c] = sm.Dt[c] * sm.qt[c];
+      sm.D[c] = sm.D[c] * sm.Dt[c];
+    }
+    // cost normalization: mean column norm of P and inf-norm of q
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int c = 3 * t + k;
-          ob += 0.5 * sm.X[c] * sm.PX[c] + sm.qt[c] * sm.X[c];
+    for (int i = 0; i < 3; ++i) {
+      double mx = 0.0;
+#pragma unroll
+      for (int j = 0; j < BC; ++j) mx = dmax(mx, dabs(M[i][j]));
+      pm[i] = g16_max(mx);
+    }
+    double sv[1] = {var_lane ? (a == 0 ? pm[0] : a == 1 ? pm[1] : pm[2]) : 0.0};
+    double qv[1] = {var_lane ? dabs(sm.qt[c]) : 0.0};
+    wg_reduce<N, 1, false>(sm, sv, rslot);
+    wg_reduce<N, 1, true>(sm, qv, rslot);
+    double c_temp = sv[0] / n;
+    const double inf_norm_q = limit_scaling(qv[0]);
+    c_temp = dmax(c_temp, inf_norm_q);
+    c_temp = limit_scaling(c_temp);
+    c_temp = 1. / c_temp;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < BC; ++j) M[i][j] *= c_temp;
+    if (var_lane) sm.qt[c] *= c_temp;
+    cost_c *= c_temp;
+  }
+  const double cinv = 1. / cost_c;
+  if (var_lane) sm.Dinv[c] = 1. / sm.D[c];
+  if (row_lane) {
+    sm.Einv[r] = 1. / sm.E[r];
+    sm.lo[r] = sm.E[r] * sm.lo[r];
+    sm.hi[r] = sm.E[r] * sm.hi[r];
+  }
+  store_tile<N>(M, Pw, f, tc);  // scaled P~ kept for rho refactorizations
+  double rho = dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
+  if (row_lane) {
+    set_row_rho<N>(sm, r, rho, true);
+    sm.z[r] = 0.0;
+    sm.y[r] = 0.0;
+  }
+  if (var_lane) {
+    compute_bd_row<N>(sm, f, a);
+    sm.x[c] = 0.0;
+    sm.px[c] = 0.0;
+  }
+  for (int e = n + t0; e < Dm::NP; e += NT) sm.rhs[0][e] = sm.rhs[1][e] = 0.0;  // padding
+
+  // ---- 3. ADMM -------------------------------------------------------------------------------
+  int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
+  double pri_res = 0.0, dua_res = 0.0;
+  // iteration-1 right-hand side from the cold start (x = z = y = 0)
+  if (var_lane) {
+    const double rr = sigma * 0.0 - sm.qt[c];
+    sm.rhs[1][c] = rr;  // read by iteration 1
+    sm.xrhs[c] = rr;
+  }
+  __syncthreads();
+  bool need_factor = true;  // K^-1 is (re)built at the top of the iteration that needs it
+  for (int iter = 1; iter <= p.max_iter; ++iter) {
+    const int t = opaque(threadIdx.x);
+    const int f = t >> 4, tc = t & 15;
+    const bool row_lane = tc < 5, var_lane = tc >= 5 && tc < 8;
+    const int r = 5 * f + tc, a = tc - 5, c = 3 * f + (a < 0 ? 0 : a);
+    if (need_factor) {  // single inlined site: initial factorization and osqp_update_rho refactors
+      if (iter > 1) load_tile<N>(M, Pw, f, tc);
+      build_and_invert<N>(M, sm, sigma);
+      need_factor = false;
+    }
+    // (b) x~ = K^-1 rhs: register-tile mat-vec, all-reduced inside the foot's 16-lane group
+    double xt[3];
+    {
+      double v[BC];
+#pragma unroll
+      for (int j = 0; j < BC; ++j) v[j] = sm.rhs[iter & 1][tc * BC + j];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < BC; ++j) acc = fma(M[i][j], v[j], acc);
+        xt[i] = g16_sum(acc);
+      }
+    }
+    const bool is_check = p.check_termination && (iter % p.check_termination == 0);
+    const bool is_adapt = p.adaptive_rho && p.adaptive_rho_interval && (iter % p.adaptive_rho_interval == 0);
+    const bool last = iter == p.max_iter;
+    const bool need_info = is_check || is_adapt || last;
+    // (c) update_z / update_y on row lanes, update_x (+ P~x via the KKT identity) on var lanes
+    double zn = 0.0, yn = 0.0, dyv = 0.0, xn = 0.0, dxv = 0.0, pxn = 0.0, pxo = 0.0;
+    double am = 0.0, az = 0.0;
+    if (row_lane) {
+      am = sm.am[r];
+      az = sm.az[r];
+      const double xm = tc < 2 ? xt[0] : tc < 4 ? xt[1] : xt[2];
+      const double ztl = tc < 4 ? am * xm + az * xt[2] : am * xt[2];
+      const double zo = sm.z[r], yo = sm.y[r];
+      const double zr = alpha * ztl + (1.0 - alpha) * zo;
+      zn = dmin(dmax(zr + sm.rho_inv[r] * yo, sm.lo[r]), sm.hi[r]);
+      dyv = sm.rho_v[r] * (zr - zn);
+      yn = yo + dyv;
+      sm.z[r] = zn;
+      sm.y[r] = yn;
+    }
+    if (var_lane) {
+      const double xta = a == 0 ? xt[0] : a == 1 ? xt[1] : xt[2];
+      const double xo = sm.x[c];
+      xn = alpha * xta + (1.0 - alpha) * xo;
+      dxv = xn - xo;
+      const double pxt = sm.xrhs[c] - sigma * xta - ((sm.BD[c][0] * xt[0] + sm.BD[c][1] * xt[1]) + sm.BD[c][2] * xt[2]);
+      pxo = sm.px[c];
+      pxn = alpha * pxt + (1.0 - alpha) * pxo;
+      sm.x[c] = xn;
+      sm.px[c] = pxn;
+    }
+    // gather helper: var lane a sums A~'v over its foot's rows from the row lanes' (am v, az v)
+    //   fx: am0 v0 + am1 v1;  fy: am2 v2 + am3 v3;  fz: az0 v0 + az1 v1 + az2 v2 + az3 v3 + am4 v4
+    const int gbase = t & ~15;
+    auto gather = [&](double cm, double cz, double init) {
+      const int s0 = gbase + (a == 1 ? 2 : 0), s1 = gbase + (a == 1 ? 3 : 1);
+      const double m0 = __shfl(cm, s0), m1 = __shfl(cm, s1);
+      const double z0 = __shfl(cz, gbase + 0), z1 = __shfl(cz, gbase + 1);
+      const double z2 = __shfl(cz, gbase + 2), z3 = __shfl(cz, gbase + 3);
+      const double m4 = __shfl(cm, gbase + 4);
+      if (a == 2) return ((((init + z0) + z1) + z2) + z3) + m4;
+      return (init + m0) + m1;
+    };
+
+    if (need_info) {
+      // ---- update_info / check_termination / adapt_rho (osqp.c, auxil.c) ----
+      // row lanes need the new x of their foot; var lanes A~'y of the new y
+      const double x0n = __shfl(xn, gbase + 5), x1n = __shfl(xn, gbase + 6), x2n = __shfl(xn, gbase + 7);
+      double ax = 0.0;
+      if (row_lane) ax = tc < 4 ? am * (tc < 2 ? x0n : x1n) + az * x2n : am * x2n;
+      const double aty = gather(am * yn, az * yn, 0.0);
+      // the 14 norms of update_info / compute_pri_tol / compute_dua_tol / compute_rho_estimate,
+      // reduced one at a time straight into LDS (keeps register pressure flat)
+      double pr = 0.0, ei = 0.0, d = 0.0, di = 0.0, q = 0.0;
+      if (row_lane) {
+        pr = ax + (-1.0) * zn;
+        ei = sm.Einv[r];
+      }
+      if (var_lane) {
+        di = sm.Dinv[c];
+        q = sm.qt[c];
+        d = (q + 1.0 * pxn) + 1.0 * aty;
+      }
+      {
+        const int lane = t & 63, wave = t >> 6;
+        auto put = [&](int k, double v) {
+          v = wave_max(v);
+          if (lane == 0) sm.info[wave][k] = v;
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        put(0, row_lane ? dabs(ei * pr) : 0.0);
+        put(1, row_lane ? dabs(pr) : 0.0);
+        put(2, row_lane ? dabs(ei * zn) : 0.0);
+        put(3, row_lane ? dabs(zn) : 0.0);
+        put(4, row_lane ? dabs(ei * ax) : 0.0);
+        put(5, row_lane ? dabs(ax) : 0.0);
+        put(6, var_lane ? dabs(di * d) : 0.0);
+        put(7, var_lane ? dabs(d) : 0.0);
+        put(8, var_lane ? dabs(di * q) : 0.0);
+        put(9, var_lane ? dabs(q) : 0.0);
+        put(10, var_lane ? dabs(di * aty) : 0.0);
+        put(11, var_lane ? dabs(aty) : 0.0);
+        put(12, var_lane ? dabs(di * pxn) : 0.0);
+        put(13, var_lane ? dabs(pxn) : 0.0);
+      }
+      __syncthreads();
+      // workgroup maxima read from LDS where they are used (not held across the check)
+      auto mx = [&](int k) {
+        double v = sm.info[0][k];
+        for (int w = 1; w < Dm::NW; ++w) v = dmax(v, sm.info[w][k]);
+        return v;
+      };
+      pri_res = mx(0);
+      dua_res = cinv * mx(6);
+      iters = iter;
+      // check_termination (osqp.c): approx=1 is the post-loop check at max_iter (eps x 10)
+      auto check = [&](bool approx) -> int {
+        double eps_abs = p.eps_abs, eps_rel = p.eps_rel, eps_pinf = p.eps_prim_inf, eps_dinf = p.eps_dual_inf;
+        if (pri_res > OSQP_INF || dua_res > OSQP_INF) return MPCQP_STATUS_NON_CVX;
+        if (approx) { eps_abs *= 10; eps_rel *= 10; eps_pinf *= 10; eps_dinf *= 10; }
+        const double eps_prim = eps_abs + eps_rel * dmax(mx(2), mx(4));
+        const bool prim_ok = pri_res < eps_prim;
+        bool prim_inf = false, dual_inf = false;
+        if (!prim_ok) {
+          // is_primal_infeasible: project delta_y onto the polar of the recession cone (in place)
+          if (row_lane) {
+            if (sm.hi[r] > OSQP_INF * MIN_SCALING) {
+              if (sm.lo[r] < -OSQP_INF * MIN_SCALING) dyv = 0.0;
+              else dyv = dmin(dyv, 0.0);
+            } else if (sm.lo[r] < -OSQP_INF * MIN_SCALING) {
+              dyv = dmax(dyv, 0.0);
+            }
+          }
+          double nd[1] = {row_lane ? dabs(sm.E[r] * dyv) : 0.0};
+          wg_reduce<N, 1, true>(sm, nd, rslot);
+          const double ndy = nd[0];
+          if (ndy > DIV_TOL) {
+            double lh[1] = {row_lane ? sm.hi[r] * dmax(dyv, 0.0) + sm.lo[r] * dmin(dyv, 0.0) : 0.0};
+            wg_reduce<N, 1, false>(sm, lh, rslot);
+            if (lh[0] < eps_pinf * ndy) {
+              const double atd = gather(am * dyv, az * dyv, 0.0);
+              double an[1] = {var_lane ? dabs(sm.Dinv[c] * atd) : 0.0};
+              wg_reduce<N, 1, true>(sm, an, rslot);
+              prim_inf = an[0] < eps_pinf * ndy;
+            }
+          }
+        }
+        const double eps_dual = eps_abs + eps_rel * (cinv * dmax(dmax(mx(8), mx(10)), mx(12)));
+        const bool dual_ok = dua_res < eps_dual;
+        if (!dual_ok) {
+          // is_dual_infeasible (P~ delta_x = P~x_new - P~x_old)
+          double nx[1] = {var_lane ? dabs(sm.D[c] * dxv) : 0.0};
+          wg_reduce<N, 1, true>(sm, nx, rslot);
+          const double ndx = nx[0];
+          if (ndx > DIV_TOL) {
+            double qd[1] = {var_lane ? q * dxv : 0.0};
+            wg_reduce<N, 1, false>(sm, qd, rslot);
+            if (qd[0] < cost_c * eps_dinf * ndx) {
+              double pd[1] = {var_lane ? dabs(sm.Dinv[c] * (pxn - pxo)) : 0.0};
+              wg_reduce<N, 1, true>(sm, pd, rslot);
+              if (pd[0] < cost_c * eps_dinf * ndx) {
+                const double dx0 = __shfl(dxv, gbase + 5), dx1 = __shfl(dxv, gbase + 6), dx2 = __shfl(dxv, gbase + 7);
+                double viol = 0.0;
+                if (row_lane) {
+                  const double adx = tc < 4 ? am * (tc < 2 ? dx0 : dx1) + az * dx2 : am * dx2;
+                  const double v = sm.Einv[r] * adx;
+                  if ((sm.hi[r] < OSQP_INF * MIN_SCALING && v > eps_dinf * ndx) ||
+                      (sm.lo[r] > -OSQP_INF * MIN_SCALING && v < -eps_dinf * ndx))
+                    viol = 1.0;
+                }
+                double vv[1] = {viol};
+                wg_reduce<N, 1, true>(sm, vv, rslot);
+                dual_inf = vv[0] == 0.0;
+              }
+            }
+          }
+        }
+        if (prim_ok && dual_ok) return approx ? MPCQP_STATUS_SOLVED_INACCURATE : MPCQP_STATUS_SOLVED;
+        if (prim_inf) return approx ? MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE : MPCQP_STATUS_PRIMAL_INFEASIBLE;
+        if (dual_inf) return approx ? MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE : MPCQP_STATUS_DUAL_INFEASIBLE;
+        return MPCQP_STATUS_UNSOLVED;
+      };
+      int st = MPCQP_STATUS_UNSOLVED;
+      bool done = false, refactor = false;
+      for (int pass = 0; pass < 2 && !done; ++pass) {
+        // pass 0: in-loop check_termination; pass 1: osqp_solve's approximate check at max_iter
+        if (pass == 1 && !last) break;
+        if (pass == 1 || is_check || last) {
+          st = check(pass == 1);
+          done = st != MPCQP_STATUS_UNSOLVED;
+        }
+        if (pass == 1 || done || !is_adapt) continue;
+        // adapt_rho / compute_rho_estimate (scaled residuals and norms); runs before the
+        // post-loop approximate check of osqp_solve
+        const double pr_n = mx(1) / (dmax(mx(3), mx(5)) + DIV_TOL);
+        const double du_n = mx(7) / (dmax(dmax(mx(9), mx(11)), mx(13)) + DIV_TOL);
+        double est = rho * sqrt(pr_n / (du_n + DIV_TOL));
+        est = dmin(dmax(est, RHO_MIN), RHO_MAX);
+        if (est > rho * p.adaptive_rho_tolerance || est < rho / p.adaptive_rho_tolerance) {
+          rho = dmin(dmax(est, RHO_MIN), RHO_MAX);
+          rho_updates += 1;
+          refactor = !last;
         }
       }
-      ob = wave_sum(ob);
-      double xs[3] = {NAN, NAN, NAN};
-      if (t < 4 && has_sol) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) xs[k] = sm.D[3 * t + k] * sm.X[3 * t + k];
+      if (last && st == MPCQP_STATUS_UNSOLVED) st = MPCQP_STATUS_MAX_ITER_REACHED;
+      if (last) done = true;
+      status = st;
+      if (trace && t == 0 && inst < trace_cap && ntrace < MPCQP_TRACE_LEN && is_check) {
+        double* tp = trace + ((size_t)inst * MPCQP_TRACE_LEN + ntrace) * 4;
+        tp[0] = iter; tp[1] = pri_res; tp[2] = dua_res; tp[3] = rho;
       }
-      if (t < 4) {
-        mpcqp_result* r = results + inst;
+      ntrace += is_check ? 1 : 0;
+      if (done) break;
+      if (refactor) {
+        // osqp_update_rho: new rho vector and A~'rho A~ blocks now; P~ reload + re-inversion at
+        // the top of the next iteration
+        if (row_lane) set_row_rho<N>(sm, r, rho, false);
+        if (var_lane) compute_bd_row<N>(sm, f, a);
+        need_factor = true;
+      }
+    }
+    // (a) next right-hand side: rhs = sigma x - q~ + A~'(rho z - y)  [compute_rhs + KKT rhs]
+    {
+      double tv = 0.0;
+      if (row_lane) {
+        am = sm.am[r];
+        az = sm.az[r];
+        tv = sm.rho_v[r] * sm.z[r] - sm.y[r];
+      }
+      const double init = var_lane ? sigma * sm.x[c] - sm.qt[c] : 0.0;
+      const double rr = gather(am * tv, az * tv, init);
+      if (var_lane) {
+        sm.rhs[(iter + 1) & 1][c] = rr;  // other buffer: slower waves may still read this one
+        sm.xrhs[c] = rr;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- 4. store_solution + unscale + compute_grf extraction (A1RobotControl.cpp:555-561) ------
+  const bool has_sol = status != MPCQP_STATUS_PRIMAL_INFEASIBLE &&
+                       status != MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE &&
+                       status != MPCQP_STATUS_DUAL_INFEASIBLE &&
+                       status != MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE && status != MPCQP_STATUS_NON_CVX;
+  {
+    // objective 1/2 x'P~x + q~'x (unscaled by cinv)
+    double ob[1] = {var_lane ? 0.5 * sm.x[c] * sm.px[c] + sm.qt[c] * sm.x[c] : 0.0};
+    wg_reduce<N, 1, false>(sm, ob, rslot);
+    const double xs = has_sol ? sm.D[c] * sm.x[c] : NAN;
+    if (solution && var_lane) solution[(size_t)inst * n + c] = xs;
+    if (f < 4) {  // horizon step 0 = feet 0..3 = legs FL, FR, RL, RR
+      mpcqp_result* res = results + inst;
+      const int gbase = t0 & ~15;
+      const double u0 = __shfl(xs, gbase + 5), u1 = __shfl(xs, gbase + 6), u2 = __shfl(xs, gbase + 7);
+      const double nrm = sqrt(u0 * u0 + u1 * u1 + u2 * u2);
+      const bool nanleg = isnan(nrm);
+      if (var_lane) {
         const double* R = sm.rec + MPCQP_REC_ROT;
-        const double nrm = sqrt(xs[0] * xs[0] + xs[1] * xs[1] + xs[2] * xs[2]);
-        const bool nanleg = isnan(nrm);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          r->u0[3 * t + k] = xs[k];
-          double s = 0.0;
-          s += R[0 * 3 + k] * xs[0];
-          s += R[1 * 3 + k] * xs[1];
-          s += R[2 * 3 + k] * xs[2];
-          r->f_body[3 * t + k] = nanleg ? 0.0 : s;
-        }
-        const unsigned long long nb = __ballot(nanleg);
-        if (t == 0) {
-          r->nan_legs = (int)(nb & 0xFull);
-          double obj;
-          if (has_sol) obj = ob * cinv;
-          else if (status == MPCQP_STATUS_PRIMAL_INFEASIBLE || status == MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE) obj = OSQP_INF;
-          else if (status == MPCQP_STATUS_DUAL_INFEASIBLE || status == MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE) obj = -OSQP_INF;
-          else obj = NAN;
-          r->obj_val = obj;
-          r->pri_res = pri_res;
-          r->dua_res = dua_res;
-          r->rho = rho;
-          r->status = status;
-          r->iters = iters;
-          r->rho_updates = rho_updates;
-        }
+        double s = 0.0;
+        s += R[0 * 3 + a] * u0;
+        s += R[1 * 3 + a] * u1;
+        s += R[2 * 3 + a] * u2;
+        res->u0[3 * f + a] = xs;
+        res->f_body[3 * f + a] = nanleg ? 0.0 : s;
       }
-    }
-    if (solution) {
-      for (int e = t; e < n; e += NT)
-        solution[(size_t)inst * n + e] = has_sol ? sm.D[e] * sm.X[e] : NAN;
+      const unsigned long long nb = __ballot(nanleg && tc == 0);
+      if (t0 == 0) {
+        int legs = 0;
+        for (int l = 0; l < 4; ++l) legs |= ((nb >> (16 * l)) & 1ull) ? (1 << l) : 0;
+        res->nan_legs = legs;
+        double obj;
+        if (has_sol) obj = ob[0] * cinv;
+        else if (status == MPCQP_STATUS_PRIMAL_INFEASIBLE || status == MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE) obj = OSQP_INF;
+        else if (status == MPCQP_STATUS_DUAL_INFEASIBLE || status == MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE) obj = -OSQP_INF;
+        else obj = NAN;
+        res->obj_val = obj;
+        res->pri_res = pri_res;
+        res->dua_res = dua_res;
+        res->rho = rho;
+        res->status = status;
+        res->iters = iters;
+        res->rho_updates = rho_updates;
+      }
     }
   }
 }
 
-// Formulation-only kernel (P0 parity): dense H (row-major n x n), g, l, u.
+// Formulation-only kernel (P0 parity / ConvexMpc shim): dense H (row-major n x n), g, l, u.
 template <int N>
 __global__ __launch_bounds__(256) void build_qp_kernel(const double* __restrict__ recs, int batch,
                                                        double* __restrict__ P, double* __restrict__ q,
@@ -1022,9 +1005,7 @@ __global__ __launch_bounds__(256) void build_qp_kernel(const double* __restrict_
 // ---- launch table --------------------------------------------------------------------------
 template <int N>
 static hipError_t launch_solve(const LaunchArgs& a) {
-  constexpr int BR = SOLVE_BR;
-  constexpr int NT = (NP / BR) * 16;
-  hipLaunchKernelGGL((solve_kernel<N, BR>), dim3(a.grid), dim3(NT), 0, (hipStream_t)a.stream, a.recs,
+  hipLaunchKernelGGL((solve_kernel<N>), dim3(a.grid), dim3(Dim<N>::NT), 0, (hipStream_t)a.stream, a.recs,
                      a.batch, a.results, a.solution, a.work, a.trace, a.trace_cap, a.p);
   return hipGetLastError();
 }
@@ -1036,9 +1017,7 @@ static hipError_t launch_build(const LaunchArgs& a, double* P, double* q, double
 }
 template <int N>
 static hipError_t occupancy(int* blocks) {
-  constexpr int BR = SOLVE_BR;
-  constexpr int NT = (NP / BR) * 16;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, solve_kernel<N, BR>, NT, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, solve_kernel<N>, Dim<N>::NT, 0);
 }
 
 #ifndef MPCQP_FOR_EACH_N
@@ -1072,6 +1051,10 @@ hipError_t occupancy_any(int horizon, int* blocks) {
     default: return hipErrorInvalidValue;
   }
 }
-int solve_threads() { return (NP / SOLVE_BR) * 16; }
+int solve_threads(int horizon) { return 16 * 4 * horizon; }
+size_t workspace_doubles(int horizon) {
+  const int n = 12 * horizon;
+  return (size_t)n * 16 * ((n + 15) / 16);
+}
 
 }  // namespace mpcqp

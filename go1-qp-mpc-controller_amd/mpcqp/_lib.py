@@ -128,7 +128,7 @@ def load():
     L.mpcqp_abi_sizes.restype = i32
     L.mpcqp_handle_slots.argtypes = [vp]
     L.mpcqp_handle_slots.restype = i32
-    L.mpcqp_solve_threads.argtypes = []
+    L.mpcqp_solve_threads.argtypes = [i32]
     L.mpcqp_solve_threads.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))

@@ -25,8 +25,8 @@ int32_t mpcqp_abi_sizes(int32_t* params_size, int32_t* result_size);
 /* Persistent-grid size (resident workgroups) chosen for the handle's device. */
 int32_t mpcqp_handle_slots(mpcqp_handle* h);
 
-/* Threads per instance workgroup of the solve kernel. */
-int32_t mpcqp_solve_threads(void);
+/* Threads per robot workgroup of the solve kernel for horizon N (one 16-lane group per foot). */
+int32_t mpcqp_solve_threads(int32_t horizon);
 
 #ifdef __cplusplus
 }

@@ -74,7 +74,7 @@ def main():
     with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
         slots = s.slots
     per = lambda ms: ms * 1e3 * min(slots, B) / B  # µs of a resident slot per instance  # noqa: E731
-    out = {"batch": B, "cus": cus, "slots": slots, "threads": mpcqp.load().mpcqp_solve_threads()}
+    out = {"batch": B, "cus": cus, "slots": slots, "threads": mpcqp.load().mpcqp_solve_threads(10)}
     A, _ = time_solve(mpcqp.default_params(10, max_iter=1, adaptive_rho=0), recs)
     Bt, _ = time_solve(mpcqp.default_params(10, max_iter=1, adaptive_rho=0, scaling=0), recs)
     C, _ = time_solve(mpcqp.default_params(10, max_iter=101, adaptive_rho=0, eps_abs=0.0, eps_rel=0.0), recs)
