@@ -42,30 +42,29 @@ struct Dim {
   static constexpr int n = ND * N, m = CD * N, nf = 4 * N, ns = SD * N;
   static constexpr int rec = MPCQP_REC_SIZE(N);
   static constexpr int feet = MPCQP_REC_FEET(N);
-  static constexpr int BC = (n + 15) / 16;  // columns per thread
-  static constexpr int NP = 16 * BC;        // padded column count
-  static constexpr int NT = 16 * nf;        // threads: one 16-lane group per foot
-  static constexpr int NW = NT / 64;        // waves
+  static constexpr int GL = 8;                                   // lanes per foot group
+  static constexpr int BC = 3 * ((n + 3 * GL - 1) / (3 * GL));   // tile columns per lane (multiple of 3)
+  static constexpr int NP = GL * BC;                             // padded column count
+  static constexpr int NT = ((GL * nf + 63) / 64) * 64;          // threads (whole waves)
+  static constexpr int NG = NT / GL;                             // groups, idle ones included
+  static constexpr int NW = NT / 64;                             // waves
+  static constexpr int SPL = BC / 3;                             // feet whose columns one lane holds
 };
 
-// LDS image of one robot.
+// LDS image of one robot.  The per-row / per-variable ADMM state lives in registers of the
+// owning lanes; LDS only carries what crosses lanes.
 template <int N>
 struct Smem {
   using Dm = Dim<N>;
   double rec[Dm::rec];
-  // constraint rows (owned by lanes 0-4 of the foot's group)
-  double z[Dm::m], y[Dm::m], lo[Dm::m], hi[Dm::m], rho_v[Dm::m], rho_inv[Dm::m];
-  double am[Dm::m], az[Dm::m];  // A~ row: coefficient on the row's main variable / on fz
-  double E[Dm::m], Einv[Dm::m];
-  int ctype[Dm::m];
-  // variables (owned by lanes 5-7)
-  double x[Dm::n], px[Dm::n], qt[Dm::n], D[Dm::n], Dinv[Dm::n], xrhs[Dm::n];
-  double BD[Dm::n][3];  // (A~' diag(rho) A~) row of each variable (3x3 block per foot)
+  double lo[Dm::m], hi[Dm::m];  // condensation output: unscaled bounds
+  double qt[Dm::n];             // condensation output: gradient
+  double rowc[Dm::m][4];        // scaled A~ row (coefficients on fx, fy, fz) and its rho
+  double BD[Dm::n][3];          // (A~' diag(rho) A~) row of each variable (3x3 block per foot)
   alignas(16) double rhs[2][Dm::NP];  // KKT right-hand side, double-buffered by iteration parity
-  alignas(16) double Dt[Dm::NP];
-  double red[2][Dm::NW][16];              // workgroup reductions (double-buffered)
-  double info[Dm::NW][16];                // per-wave maxima of the termination / rho norms
-  double cst[4];                          // 0: c, 1: cinv
+  alignas(16) double Dt[Dm::NP];      // Ruiz D_temp
+  double red[2][Dm::NW][16];          // workgroup reductions (double-buffered)
+  double info[Dm::NW][16];            // per-wave maxima of the termination / rho norms
   union U {
     struct C {
       double S[N][SD * SD];
@@ -77,10 +76,10 @@ struct Smem {
       double a[SD];
       double w[SD];
     } c;
-    struct G {  // block Gauss-Jordan broadcast lines (double-buffered)
+    struct G {  // block Gauss-Jordan broadcast lines (double-buffered by pivot parity)
       alignas(16) double r[2][3][Dm::NP];  // P^-1 * pivot rows
-      double c[2][Dm::n][3];               // pivot columns
-      double p[2][9];                      // P^-1 (raw pivot block before phase A ends)
+      double ck[2][Dm::NG][9];             // every group's 3x3 block of the pivot columns
+      double pinv[2][9];                   // P^-1
     } g;
   } u;
 };
@@ -93,7 +92,12 @@ __device__ __forceinline__ int opaque(int v) {
 }
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
-__device__ __forceinline__ double dabs(double a) { return a < 0 ? -a : a; }
+__device__ __forceinline__ double dabs(double a) { return __builtin_fabs(a); }
+// Three-way select on values (a select of lvalues can become a select of addresses, which
+// forces the operands out of registers into scratch).
+__device__ __forceinline__ double sel3(int k, double a, double b, double c) {
+  return k == 0 ? a : (k == 1 ? b : c);
+}
 __device__ __forceinline__ double limit_scaling(double d) {
   d = d < MIN_SCALING ? 1.0 : d;
   return d > MAX_SCALING ? MAX_SCALING : d;
@@ -123,6 +127,25 @@ __device__ __forceinline__ double g16_max(double v) {
   v = dmax(v, dpp<0x4E>(v));
   v = dmax(v, dpp<0xB1>(v));
   return v;
+}
+// 8-lane (foot group) all-reduce, same bitwise-symmetric pairing argument as g16_*.
+__device__ __forceinline__ double g8_sum(double v) {
+  v = v + dpp<0x141>(v);
+  v = v + dpp<0x4E>(v);
+  v = v + dpp<0xB1>(v);
+  return v;
+}
+__device__ __forceinline__ double g8_max(double v) {
+  v = dmax(v, dpp<0x141>(v));
+  v = dmax(v, dpp<0x4E>(v));
+  v = dmax(v, dpp<0xB1>(v));
+  return v;
+}
+// Orders LDS traffic between lanes of one wave (LDS executes a wave's operations in order; this
+// keeps the compiler from moving memory operations across the hand-off).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ double wave_max(double v) {
   v = g16_max(v);
@@ -336,7 +359,7 @@ __device__ __forceinline__ void condense(Smem<N>& sm, const mpcqp_params& p, dou
   __syncthreads();
 }
 
-// ---- register tile: rows 3f..3f+2 (the foot's variables) x cols tc*BC .. tc*BC+BC-1 ----------
+// ---- register tile: rows 3f..3f+2 (foot f's forces) x cols tc*BC .. tc*BC+BC-1 ----------------
 template <int N>
 __device__ __forceinline__ void load_tile(double (&M)[3][Dim<N>::BC], const double* __restrict__ P, int f,
                                           int tc) {
@@ -347,7 +370,7 @@ __device__ __forceinline__ void load_tile(double (&M)[3][Dim<N>::BC], const doub
 #pragma unroll
     for (int j = 0; j < Dm::BC; ++j) {
       const int c = tc * Dm::BC + j;
-      M[i][j] = (c < Dm::n) ? P[(size_t)r * Dm::NP + c] : 0.0;
+      M[i][j] = (r < Dm::n && c < Dm::n) ? P[(size_t)r * Dm::NP + c] : 0.0;
     }
   }
 }
@@ -361,82 +384,82 @@ __device__ __forceinline__ void store_tile(const double (&M)[3][Dim<N>::BC], dou
 #pragma unroll
     for (int j = 0; j < Dm::BC; ++j) {
       const int c = tc * Dm::BC + j;
-      if (c < Dm::n) P[(size_t)r * Dm::NP + c] = M[i][j];
+      if (r < Dm::n && c < Dm::n) P[(size_t)r * Dm::NP + c] = M[i][j];
     }
   }
 }
 
-// A~' diag(rho) A~ rows for variable lanes (role a = tc - 5 of group f), from the row data of the
-// same group (same wave: LDS ordering, no barrier).
+// Workgroup sum of s and max of mx in one round trip.
 template <int N>
-__device__ __forceinline__ void compute_bd_row(Smem<N>& sm, int f, int a) {
-  const int r0 = 5 * f;
-  const double* am = sm.am + r0;
-  const double* az = sm.az + r0;
-  const double* rv = sm.rho_v + r0;
-  double b0, b1, b2;
-  if (a == 0) {  // fx: rows 0,1 (main), fz coupling via az
-    b0 = am[0] * rv[0] * am[0] + am[1] * rv[1] * am[1];
-    b1 = 0.0;
-    b2 = am[0] * rv[0] * az[0] + am[1] * rv[1] * az[1];
-  } else if (a == 1) {  // fy: rows 2,3
-    b0 = 0.0;
-    b1 = am[2] * rv[2] * am[2] + am[3] * rv[3] * am[3];
-    b2 = am[2] * rv[2] * az[2] + am[3] * rv[3] * az[3];
-  } else {  // fz: az of rows 0-3 and the main coefficient of row 4
-    b0 = am[0] * rv[0] * az[0] + am[1] * rv[1] * az[1];
-    b1 = am[2] * rv[2] * az[2] + am[3] * rv[3] * az[3];
-    b2 = az[0] * rv[0] * az[0] + az[1] * rv[1] * az[1] + az[2] * rv[2] * az[2] + az[3] * rv[3] * az[3] +
-         am[4] * rv[4] * am[4];
-  }
-  const int c = 3 * f + a;
-  sm.BD[c][0] = b0;
-  sm.BD[c][1] = b1;
-  sm.BD[c][2] = b2;
-}
-
-// set_rho_vec (auxil.c) for the row lane (row r); on reclassify also decides the constraint type.
-template <int N>
-__device__ __forceinline__ void set_row_rho(Smem<N>& sm, int r, double rho, bool reclassify) {
-  int ct;
-  if (reclassify) {
-    if (sm.lo[r] < -OSQP_INF * MIN_SCALING && sm.hi[r] > OSQP_INF * MIN_SCALING)
-      ct = -1;
-    else if (sm.hi[r] - sm.lo[r] < RHO_TOL)
-      ct = 1;
-    else
-      ct = 0;
-    sm.ctype[r] = ct;
-  } else {
-    ct = sm.ctype[r];
-  }
-  double rr;
-  if (ct == -1)
-    rr = reclassify ? RHO_MIN : sm.rho_v[r];
-  else if (ct == 1)
-    rr = RHO_EQ_OVER_RHO_INEQ * rho;
-  else
-    rr = rho;
-  sm.rho_v[r] = rr;
-  sm.rho_inv[r] = 1. / rr;
-}
-
-// K = P~ + sigma I + A~' rho A~ from the tile already holding P~, then its inverse by block
-// Gauss-Jordan with 3x3 pivot blocks (pivot block kf = foot kf's diagonal block):
-//   A_kk <- P^-1,  A_kj <- P^-1 A_kj,  A_ik <- -A_ik P^-1,  A_ij <- A_ij - A_ik P^-1 A_kj.
-template <int N>
-__device__ __forceinline__ void build_and_invert(double (&M)[3][Dim<N>::BC], Smem<N>& sm, double sigma) {
+__device__ __forceinline__ void wg_sum_max(Smem<N>& sm, double& s, double& mx, int& slot) {
   using Dm = Dim<N>;
-  constexpr int BC = Dm::BC, n = Dm::n;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  s = wave_sum(s);
+  mx = wave_max(mx);
+  if (lane == 0) {
+    sm.red[slot][wave][0] = s;
+    sm.red[slot][wave][1] = mx;
+  }
+  __syncthreads();
+  double rs = sm.red[slot][0][0], rm = sm.red[slot][0][1];
+  for (int w = 1; w < Dm::NW; ++w) {
+    rs = rs + sm.red[slot][w][0];
+    rm = dmax(rm, sm.red[slot][w][1]);
+  }
+  s = rs;
+  mx = rm;
+  slot ^= 1;
+}
+
+// (A~' diag(rho) A~) row of variable 3f+a from the foot's five rows (sm.rowc, written by the
+// row lanes of the same group = same wave).
+template <int N>
+__device__ __forceinline__ void bd_row(const Smem<N>& sm, int f, int a, double& b0, double& b1, double& b2) {
+  b0 = 0.0;
+  b1 = 0.0;
+  b2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const double* rc = sm.rowc[5 * f + k];
+    const double w = sel3(a, rc[0], rc[1], rc[2]) * rc[3];
+    b0 += w * rc[0];
+    b1 += w * rc[1];
+    b2 += w * rc[2];
+  }
+}
+
+// A~'v at the variable lanes of each foot group from the row lanes' mv = (main coefficient) v and
+// zv = (fz coefficient) v, with DPP row shifts, in the reference's summation order:
+//   fx: m0 + m1,  fy: m2 + m3,  fz: z0 + z1 + z2 + z3 + m4   (rows 0-4 of the foot).
+// Must be called with every lane of the wave active.
+__device__ __forceinline__ double gather_atv(double mv, double zv, int a, double init) {
+  const double m3 = dpp<0x113>(mv), m4 = dpp<0x114>(mv), m5 = dpp<0x115>(mv);
+  const double z4 = dpp<0x114>(zv), z5 = dpp<0x115>(zv), z6 = dpp<0x116>(zv), z7 = dpp<0x117>(zv);
+  const double s1 = sel3(a, m5, m4, z7);
+  const double s2 = sel3(a, m4, m3, z6);
+  const double acc = (init + s1) + s2;
+  const double accz = ((acc + z5) + z4) + m3;
+  return a == 2 ? accz : acc;
+}
+
+// K = P~ + sigma I + blockdiag(A~' rho A~) from the tile holding P~, then K^-1 in place by block
+// Gauss-Jordan with the 3x3 diagonal block of foot kf as pivot:
+//   A_kk <- P^-1,  A_kj <- P^-1 A_kj,  A_ik <- -A_ik P^-1,  A_ij <- A_ij - A_ik P^-1 A_kj.
+// Pivot kf's columns 3kf..3kf+2 are tile columns 3s..3s+2 of lane L = kf / SPL (s = kf % SPL);
+// unrolling s makes them static register positions.
+template <int N>
+__device__ __forceinline__ void factor_and_invert(double (&M)[3][Dim<N>::BC], Smem<N>& sm, double sigma) {
+  using Dm = Dim<N>;
+  constexpr int BC = Dm::BC, n = Dm::n, SPL = Dm::SPL;
   const int t = opaque(threadIdx.x);
-  const int f = t >> 4, tc = t & 15;
+  const int f = t >> 3, tc = t & 7;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int r = 3 * f + i;
 #pragma unroll
     for (int j = 0; j < BC; ++j) {
       const int c = tc * BC + j;
-      if (c < n) {
+      if (r < n && c < n) {
         double v = M[i][j];
         if (r == c) v += sigma;
         if (c / 3 == f) v += sm.BD[r][c - 3 * f];
@@ -444,87 +467,106 @@ __device__ __forceinline__ void build_and_invert(double (&M)[3][Dim<N>::BC], Sme
       }
     }
   }
-  for (int kf = 0; kf < Dm::nf; ++kf) {
-    const int b = kf & 1;
-    // ---- phase A: the pivot group publishes P^-1 A_k. and the raw pivot columns ----
-    if (f == kf) {
-      // pivot block P = M[0..2][3kf..3kf+2] lives in 1-2 lanes of this group: publish via LDS
+  for (int L = 0; L < (Dm::nf + SPL - 1) / SPL; ++L) {
 #pragma unroll
-      for (int j = 0; j < BC; ++j) {
-        const int c = tc * BC + j;
-        if (c >= 3 * kf && c < 3 * kf + 3)
+    for (int s = 0; s < SPL; ++s) {
+      const int kf = L * SPL + s;
+      if (kf >= Dm::nf) break;
+      const int b = kf & 1;
+      const bool piv = f == kf;   // this group owns the pivot rows
+      const bool pl = tc == L;    // this lane holds the pivot columns
+      // ---- phase A: pivot columns of every group, P^-1, and P^-1 A_k. ----
+      if (pl) {
 #pragma unroll
-          for (int i = 0; i < 3; ++i) sm.u.g.p[b][i * 3 + (c - 3 * kf)] = M[i][j];
-      }
-      double P[9];
+        for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int e = 0; e < 9; ++e) P[e] = sm.u.g.p[b][e];  // same wave: ordered after the stores
-      auto cof = [&](int i, int j) {
-        const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-        return P[i1 * 3 + j1] * P[i2 * 3 + j2] - P[i1 * 3 + j2] * P[i2 * 3 + j1];
-      };
-      const double det = (cof(0, 0) * P[0] + cof(1, 0) * P[3]) + cof(2, 0) * P[6];
-      const double invdet = 1.0 / det;
-      double Pi[9];
+          for (int q = 0; q < 3; ++q) sm.u.g.ck[b][f][3 * i + q] = M[i][3 * s + q];
+        if (piv) {
+          double P[9];
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+          for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) Pi[j * 3 + i] = cof(i, j) * invdet;
+            for (int q = 0; q < 3; ++q) P[3 * i + q] = M[i][3 * s + q];
+          auto cof = [&](int i, int j) {
+            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            return P[i1 * 3 + j1] * P[i2 * 3 + j2] - P[i1 * 3 + j2] * P[i2 * 3 + j1];
+          };
+          const double det = (cof(0, 0) * P[0] + cof(1, 0) * P[3]) + cof(2, 0) * P[6];
+          const double invdet = 1.0 / det;
 #pragma unroll
-      for (int j = 0; j < BC; ++j) {
-        const double r0 = M[0][j], r1 = M[1][j], r2 = M[2][j];
+          for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int i = 0; i < 3; ++i) sm.u.g.r[b][i][tc * BC + j] = (Pi[i * 3] * r0 + Pi[i * 3 + 1] * r1) + Pi[i * 3 + 2] * r2;
-      }
-      if (tc == 0) {
-#pragma unroll
-        for (int e = 0; e < 9; ++e) sm.u.g.p[b][e] = Pi[e];
-      }
-    }
-    // pivot columns: every group's lanes holding cols 3kf..3kf+2 publish their 3 rows
-#pragma unroll
-    for (int j = 0; j < BC; ++j) {
-      const int c = tc * BC + j;
-      if (c >= 3 * kf && c < 3 * kf + 3)
-#pragma unroll
-        for (int i = 0; i < 3; ++i) sm.u.g.c[b][3 * f + i][c - 3 * kf] = M[i][j];
-    }
-    __syncthreads();
-    // ---- phase B: rank-3 update of every tile, then the pivot row/column fix-ups ----
-    double Ck[3][3], Pi[9];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) Ck[i][q] = sm.u.g.c[b][3 * f + i][q];
-#pragma unroll
-    for (int e = 0; e < 9; ++e) Pi[e] = sm.u.g.p[b][e];
-    const bool own_row = f == kf;
-#pragma unroll
-    for (int j = 0; j < BC; ++j) {
-      const int c = tc * BC + j;
-      const double R0 = sm.u.g.r[b][0][c], R1 = sm.u.g.r[b][1][c], R2 = sm.u.g.r[b][2][c];
-      const bool kcol = c >= 3 * kf && c < 3 * kf + 3;
-      const int q = c - 3 * kf;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        double v;
-        // column q of P^-1 selected without a runtime register index
-        const double p0 = q == 0 ? Pi[0] : q == 1 ? Pi[1] : Pi[2];
-        const double p1 = q == 0 ? Pi[3] : q == 1 ? Pi[4] : Pi[5];
-        const double p2 = q == 0 ? Pi[6] : q == 1 ? Pi[7] : Pi[8];
-        if (own_row) {
-          v = kcol ? (i == 0 ? p0 : i == 1 ? p1 : p2) : (i == 0 ? R0 : i == 1 ? R1 : R2);
-        } else if (kcol) {
-          v = -((Ck[i][0] * p0 + Ck[i][1] * p1) + Ck[i][2] * p2);
-        } else {
-          v = M[i][j] - ((Ck[i][0] * R0 + Ck[i][1] * R1) + Ck[i][2] * R2);
+            for (int j = 0; j < 3; ++j) sm.u.g.pinv[b][j * 3 + i] = cof(i, j) * invdet;
         }
-        M[i][j] = v;
+      }
+      if (piv) {
+        wave_sync();
+        double Pi[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Pi[e] = sm.u.g.pinv[b][e];
+#pragma unroll
+        for (int j = 0; j < BC; ++j) {
+          const double r0 = M[0][j], r1 = M[1][j], r2 = M[2][j];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const double v = (Pi[i * 3] * r0 + Pi[i * 3 + 1] * r1) + Pi[i * 3 + 2] * r2;
+            sm.u.g.r[b][i][tc * BC + j] = v;
+            M[i][j] = v;
+          }
+        }
+        if (pl) {
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) M[i][3 * s + q] = Pi[i * 3 + q];
+        }
+      }
+      __syncthreads();
+      // ---- phase B: rank-3 update of every other group's rows ----
+      if (!piv) {
+        double Ck[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Ck[e] = sm.u.g.ck[b][f][e];
+#pragma unroll
+        for (int j = 0; j < BC; ++j) {
+          const int c = tc * BC + j;
+          const double R0 = sm.u.g.r[b][0][c], R1 = sm.u.g.r[b][1][c], R2 = sm.u.g.r[b][2][c];
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+            M[i][j] = M[i][j] - ((Ck[i * 3] * R0 + Ck[i * 3 + 1] * R1) + Ck[i * 3 + 2] * R2);
+        }
+        double Pv[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Pv[e] = sm.u.g.pinv[b][e];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const double w = -((Ck[i * 3] * Pv[q] + Ck[i * 3 + 1] * Pv[3 + q]) + Ck[i * 3 + 2] * Pv[6 + q]);
+            M[i][3 * s + q] = pl ? w : M[i][3 * s + q];
+          }
       }
     }
   }
   __syncthreads();
 }
+
+// Phase timing (debug builds with -DMPCQP_PHASE_TIMING): thread 0 of each traced robot appends
+// {phase id, s_memtime} pairs to the trace buffer instead of termination-check records.
+#ifdef MPCQP_PHASE_TIMING
+#define PHASE_MARK(id)                                                                     \
+  do {                                                                                     \
+    if (trace && threadIdx.x == 0 && inst < trace_cap && nmark < MPCQP_TRACE_LEN * 2) {    \
+      trace[(size_t)inst * MPCQP_TRACE_LEN * 4 + 2 * nmark] = (id);                        \
+      trace[(size_t)inst * MPCQP_TRACE_LEN * 4 + 2 * nmark + 1] = (double)__builtin_readcyclecounter(); \
+      ++nmark;                                                                             \
+    }                                                                                      \
+  } while (0)
+#else
+#define PHASE_MARK(id) \
+  do {                 \
+  } while (0)
+#endif
 
 // ---- the solver kernel ---------------------------------------------------------------------
 template <int N>
@@ -533,7 +575,7 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
     double* __restrict__ solution, double* __restrict__ work, double* __restrict__ trace, int trace_cap,
     mpcqp_params p) {
   using Dm = Dim<N>;
-  constexpr int NT = Dm::NT, BC = Dm::BC, n = Dm::n, m = Dm::m, nf = Dm::nf;
+  constexpr int NT = Dm::NT, BC = Dm::BC, n = Dm::n, nf = Dm::nf;
   __shared__ Smem<N> sm;
   const int inst = blockIdx.x;
   if (inst >= batch) return;
@@ -542,6 +584,10 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
   const double alpha = p.alpha, sigma = p.sigma;
   double M[3][BC];
   int rslot = 0;
+#ifdef MPCQP_PHASE_TIMING
+  int nmark = 0;
+#endif
+  PHASE_MARK(0);
 
   // ---- 0. record -> LDS, non-finite guard --------------------------------------------------
   {
@@ -567,23 +613,46 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
   }
 
   // ---- 1. condensation -> workspace (unscaled H), sm.qt (gradient), sm.lo/hi ----------------
+  PHASE_MARK(1);
   condense<N, NT>(sm, p, Pw, Dm::NP);
+  PHASE_MARK(2);
 
-  const int f = t0 >> 4, tc = t0 & 15;
-  const bool row_lane = tc < 5, var_lane = tc >= 5 && tc < 8;
-  const int r = 5 * f + tc;        // constraint row of a row lane
-  const int a = tc - 5;            // variable role of a var lane
-  const int c = 3 * f + (a < 0 ? 0 : a);  // variable of a var lane
+  // Lane roles inside foot group f: lanes 0-4 own the foot's friction-pyramid rows r = 5f+tc,
+  // lanes 5-7 its force variables c = 3f+a.  The two roles share the state registers below.
+  const int f = t0 >> 3, tc = t0 & 7;
+  const bool live = f < nf;
+  const bool row_lane = live && tc < 5, var_lane = live && tc >= 5;
+  const int r = 5 * f + tc;
+  const int a = tc - 5;
+  const int c = 3 * f + (a < 0 ? 0 : a);
+  double s_a = 0.0, s_b = 0.0, s_c = 0.0, s_d = 0.0, s_e = 0.0, s_f = 0.0, s_g = 0.0, s_h = 0.0;
+  double k0 = 0.0, k1 = 0.0, k2 = 0.0;  // row: A~ coefficients on (fx, fy, fz); var: A~'rho A~ row
+  double &z = s_a, &x = s_a;            // z / x
+  double &y = s_b, &px = s_b;           // y / P~x
+  double &lo = s_c, &q = s_c;           // l~ / q~
+  double &hi = s_d, &xr = s_d;          // u~ / current KKT right-hand side entry
+  double &rho_r = s_e, &rinv = s_f;     // rho of the row and its inverse
+  double &E = s_g, &D = s_g;            // Ruiz row / column scaling
+  double &Ei = s_h, &Di = s_h;          // their inverses
+  int ct = 0;                           // constraint type (set_rho_vec)
 
   // ---- 2. OSQP scale_data (Ruiz), P in registers ---------------------------------------------
   load_tile<N>(M, Pw, f, tc);
+  for (int e = n + t0; e < Dm::NP; e += NT) sm.Dt[e] = 1.0;
   if (row_lane) {  // unscaled friction pyramid row (ConvexMpc.cpp:46-58)
     const double mu = sm.rec[MPCQP_REC_MU];
-    sm.am[r] = 1.0;
-    sm.az[r] = tc == 4 ? 0.0 : ((tc & 1) ? -mu : mu);
-    sm.E[r] = 1.0;
+    const double am = 1.0, az = tc == 4 ? 0.0 : ((tc & 1) ? -mu : mu);
+    k0 = tc < 2 ? am : 0.0;
+    k1 = (tc == 2 || tc == 3) ? am : 0.0;
+    k2 = tc < 4 ? az : am;
+    E = 1.0;
+    lo = sm.lo[r];
+    hi = sm.hi[r];
   }
-  if (var_lane) sm.D[c] = 1.0;
+  if (var_lane) {
+    D = 1.0;
+    q = sm.qt[c];
+  }
   double cost_c = 1.0;
   for (int pass = 0; pass < p.scaling; ++pass) {
     // D_temp: column inf-norm of [P; A] per variable (P symmetric: row norms of the tiles)
@@ -592,21 +661,19 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
     for (int i = 0; i < 3; ++i) {
       double mx = 0.0;
 #pragma unroll
-      for (int j = 0; j < BC; ++j) mx = dmax(mx, dabs(M[i][j]));
-      pm[i] = g16_max(mx);
+      for (int j = 0; j < BC; ++j) mx = fmax(mx, dabs(M[i][j]));
+      pm[i] = g8_max(mx);
     }
+    const double ca0 = g8_max(row_lane ? dabs(k0) : 0.0);
+    const double ca1 = g8_max(row_lane ? dabs(k1) : 0.0);
+    const double ca2 = g8_max(row_lane ? dabs(k2) : 0.0);
     if (var_lane) {
-      const int r0 = 5 * f;
-      double ca;
-      if (a == 0) ca = dmax(dabs(sm.am[r0]), dabs(sm.am[r0 + 1]));
-      else if (a == 1) ca = dmax(dabs(sm.am[r0 + 2]), dabs(sm.am[r0 + 3]));
-      else ca = dmax(dmax(dmax(dmax(dabs(sm.az[r0]), dabs(sm.az[r0 + 1])), dabs(sm.az[r0 + 2])), dabs(sm.az[r0 + 3])),
-                     dabs(sm.am[r0 + 4]));
-      const double pc = a == 0 ? pm[0] : a == 1 ? pm[1] : pm[2];
-      sm.Dt[c] = 1.0 / sqrt(limit_scaling(dmax(pc, ca)));
+      const double pc = sel3(a, pm[0], pm[1], pm[2]);
+      const double cav = sel3(a, ca0, ca1, ca2);
+      sm.Dt[c] = 1.0 / sqrt(limit_scaling(dmax(pc, cav)));
     }
     double et = 1.0;
-    if (row_lane) et = 1.0 / sqrt(limit_scaling(tc == 4 ? dabs(sm.am[r]) : dmax(dabs(sm.am[r]), dabs(sm.az[r]))));
+    if (row_lane) et = 1.0 / sqrt(limit_scaling(dmax(dmax(dabs(k0), dabs(k1)), dabs(k2))));
     __syncthreads();
     // P <- D P D (premultiply by the row of the upper-triangle entry, then its column)
     double drow[3];
@@ -625,29 +692,29 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
       }
     }
     if (row_lane) {  // A <- E A D
-      const int mainv = 3 * f + (tc < 2 ? 0 : tc < 4 ? 1 : 2);
-      sm.am[r] = (sm.am[r] * et) * sm.Dt[mainv];
-      if (tc < 4) sm.az[r] = (sm.az[r] * et) * sm.Dt[3 * f + 2];
-      sm.E[r] *= et;
+      k0 = (k0 * et) * drow[0];
+      k1 = (k1 * et) * drow[1];
+      k2 = (k2 * et) * drow[2];
+      E *= et;
     }
     if (var_lane) {
-      sm.qt[c] = sm.Dt[c] * sm.qt[c];
-      sm.D[c] = sm.D[c] * sm.Dt[c];
+      const double dt = sel3(a, drow[0], drow[1], drow[2]);
+      q = dt * q;
+      D = D * dt;
     }
     // cost normalization: mean column norm of P and inf-norm of q
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       double mx = 0.0;
 #pragma unroll
-      for (int j = 0; j < BC; ++j) mx = dmax(mx, dabs(M[i][j]));
-      pm[i] = g16_max(mx);
+      for (int j = 0; j < BC; ++j) mx = fmax(mx, dabs(M[i][j]));
+      pm[i] = g8_max(mx);
     }
-    double sv[1] = {var_lane ? (a == 0 ? pm[0] : a == 1 ? pm[1] : pm[2]) : 0.0};
-    double qv[1] = {var_lane ? dabs(sm.qt[c]) : 0.0};
-    wg_reduce<N, 1, false>(sm, sv, rslot);
-    wg_reduce<N, 1, true>(sm, qv, rslot);
-    double c_temp = sv[0] / n;
-    const double inf_norm_q = limit_scaling(qv[0]);
+    double sv = var_lane ? sel3(a, pm[0], pm[1], pm[2]) : 0.0;
+    double qv = var_lane ? dabs(q) : 0.0;
+    wg_sum_max<N>(sm, sv, qv, rslot);
+    double c_temp = sv / n;
+    const double inf_norm_q = limit_scaling(qv);
     c_temp = dmax(c_temp, inf_norm_q);
     c_temp = limit_scaling(c_temp);
     c_temp = 1. / c_temp;
@@ -655,128 +722,140 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < BC; ++j) M[i][j] *= c_temp;
-    if (var_lane) sm.qt[c] *= c_temp;
+    if (var_lane) q *= c_temp;
     cost_c *= c_temp;
   }
   const double cinv = 1. / cost_c;
-  if (var_lane) sm.Dinv[c] = 1. / sm.D[c];
+  if (var_lane) Di = 1. / D;
   if (row_lane) {
-    sm.Einv[r] = 1. / sm.E[r];
-    sm.lo[r] = sm.E[r] * sm.lo[r];
-    sm.hi[r] = sm.E[r] * sm.hi[r];
+    Ei = 1. / E;
+    lo = E * lo;
+    hi = E * hi;
   }
+  PHASE_MARK(3);
   store_tile<N>(M, Pw, f, tc);  // scaled P~ kept for rho refactorizations
   double rho = dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
-  if (row_lane) {
-    set_row_rho<N>(sm, r, rho, true);
-    sm.z[r] = 0.0;
-    sm.y[r] = 0.0;
+  if (row_lane) {  // set_rho_vec (auxil.c)
+    if (lo < -OSQP_INF * MIN_SCALING && hi > OSQP_INF * MIN_SCALING)
+      ct = -1;
+    else if (hi - lo < RHO_TOL)
+      ct = 1;
+    else
+      ct = 0;
+    rho_r = ct == -1 ? RHO_MIN : ct == 1 ? RHO_EQ_OVER_RHO_INEQ * rho : rho;
+    rinv = 1. / rho_r;
+    sm.rowc[r][0] = k0;
+    sm.rowc[r][1] = k1;
+    sm.rowc[r][2] = k2;
+    sm.rowc[r][3] = rho_r;
+    z = 0.0;
+    y = 0.0;
   }
+  wave_sync();
   if (var_lane) {
-    compute_bd_row<N>(sm, f, a);
-    sm.x[c] = 0.0;
-    sm.px[c] = 0.0;
+    bd_row<N>(sm, f, a, k0, k1, k2);
+    sm.BD[c][0] = k0;
+    sm.BD[c][1] = k1;
+    sm.BD[c][2] = k2;
+    x = 0.0;
+    px = 0.0;
   }
-  for (int e = n + t0; e < Dm::NP; e += NT) sm.rhs[0][e] = sm.rhs[1][e] = 0.0;  // padding
 
   // ---- 3. ADMM -------------------------------------------------------------------------------
   int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
   double pri_res = 0.0, dua_res = 0.0;
   // iteration-1 right-hand side from the cold start (x = z = y = 0)
+  for (int e = n + t0; e < Dm::NP; e += NT) sm.rhs[0][e] = sm.rhs[1][e] = 0.0;  // padding
   if (var_lane) {
-    const double rr = sigma * 0.0 - sm.qt[c];
-    sm.rhs[1][c] = rr;  // read by iteration 1
-    sm.xrhs[c] = rr;
+    xr = sigma * 0.0 - q;
+    sm.rhs[1][c] = xr;  // read by iteration 1
   }
   __syncthreads();
   bool need_factor = true;  // K^-1 is (re)built at the top of the iteration that needs it
+  int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;  // iter % k countdowns
   for (int iter = 1; iter <= p.max_iter; ++iter) {
     const int t = opaque(threadIdx.x);
-    const int f = t >> 4, tc = t & 15;
-    const bool row_lane = tc < 5, var_lane = tc >= 5 && tc < 8;
-    const int r = 5 * f + tc, a = tc - 5, c = 3 * f + (a < 0 ? 0 : a);
+    const int f = t >> 3, tc = t & 7;
+    const bool live = f < nf;
+    const bool row_lane = live && tc < 5, var_lane = live && tc >= 5;
+    const int a = tc - 5, c = 3 * f + (a < 0 ? 0 : a);
+    const int gb = t & ~7;
     if (need_factor) {  // single inlined site: initial factorization and osqp_update_rho refactors
+      PHASE_MARK(10);
       if (iter > 1) load_tile<N>(M, Pw, f, tc);
-      build_and_invert<N>(M, sm, sigma);
+      PHASE_MARK(11);
+      factor_and_invert<N>(M, sm, sigma);
+      PHASE_MARK(12);
       need_factor = false;
     }
-    // (b) x~ = K^-1 rhs: register-tile mat-vec, all-reduced inside the foot's 16-lane group
-    double xt[3];
+    // (b) x~ = K^-1 rhs: register-tile mat-vec, all-reduced inside the foot's 8-lane group
+    double xt0, xt1, xt2;
     {
-      double v[BC];
+      const double* rb = sm.rhs[iter & 1] + tc * BC;
+      double e0 = 0.0, e1 = 0.0, e2 = 0.0, o0 = 0.0, o1 = 0.0, o2 = 0.0;
 #pragma unroll
-      for (int j = 0; j < BC; ++j) v[j] = sm.rhs[iter & 1][tc * BC + j];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < BC; ++j) acc = fma(M[i][j], v[j], acc);
-        xt[i] = g16_sum(acc);
+      for (int j = 0; j < BC; j += 2) {
+        const double v = rb[j];
+        e0 = fma(M[0][j], v, e0);
+        e1 = fma(M[1][j], v, e1);
+        e2 = fma(M[2][j], v, e2);
+        if (j + 1 < BC) {
+          const double w = rb[j + 1];
+          o0 = fma(M[0][j + 1], w, o0);
+          o1 = fma(M[1][j + 1], w, o1);
+          o2 = fma(M[2][j + 1], w, o2);
+        }
       }
+      xt0 = g8_sum(e0 + o0);
+      xt1 = g8_sum(e1 + o1);
+      xt2 = g8_sum(e2 + o2);
     }
-    const bool is_check = p.check_termination && (iter % p.check_termination == 0);
-    const bool is_adapt = p.adaptive_rho && p.adaptive_rho_interval && (iter % p.adaptive_rho_interval == 0);
+    bool is_check = false, is_adapt = false;
+    if (p.check_termination && --to_check == 0) {
+      is_check = true;
+      to_check = p.check_termination;
+    }
+    if (p.adaptive_rho && --to_adapt == 0) {
+      is_adapt = true;
+      to_adapt = p.adaptive_rho_interval;
+    }
     const bool last = iter == p.max_iter;
     const bool need_info = is_check || is_adapt || last;
-    // (c) update_z / update_y on row lanes, update_x (+ P~x via the KKT identity) on var lanes
-    double zn = 0.0, yn = 0.0, dyv = 0.0, xn = 0.0, dxv = 0.0, pxn = 0.0, pxo = 0.0;
-    double am = 0.0, az = 0.0;
+    // (c) update_z / update_y on row lanes, update_x (+ P~x via the KKT identity
+    //     P~x~ = rhs - sigma x~ - A~'rho A~ x~) on variable lanes
+    const double kd = (k0 * xt0 + k1 * xt1) + k2 * xt2;  // row: (A~x~)_r; var: (A~'rho A~ x~)_c
+    const double km = tc < 2 ? k0 : tc < 4 ? k1 : k2;    // row: coefficient on its main force
+    const double kz = tc < 4 ? k2 : 0.0;                 // row: coefficient on fz (rows 0-3)
+    double dyv = 0.0, dxv = 0.0, pxo = 0.0;
     if (row_lane) {
-      am = sm.am[r];
-      az = sm.az[r];
-      const double xm = tc < 2 ? xt[0] : tc < 4 ? xt[1] : xt[2];
-      const double ztl = tc < 4 ? am * xm + az * xt[2] : am * xt[2];
-      const double zo = sm.z[r], yo = sm.y[r];
-      const double zr = alpha * ztl + (1.0 - alpha) * zo;
-      zn = dmin(dmax(zr + sm.rho_inv[r] * yo, sm.lo[r]), sm.hi[r]);
-      dyv = sm.rho_v[r] * (zr - zn);
-      yn = yo + dyv;
-      sm.z[r] = zn;
-      sm.y[r] = yn;
+      const double zr = alpha * kd + (1.0 - alpha) * z;
+      const double zn = dmin(dmax(zr + rinv * y, lo), hi);
+      dyv = rho_r * (zr - zn);
+      y = y + dyv;
+      z = zn;
     }
     if (var_lane) {
-      const double xta = a == 0 ? xt[0] : a == 1 ? xt[1] : xt[2];
-      const double xo = sm.x[c];
-      xn = alpha * xta + (1.0 - alpha) * xo;
-      dxv = xn - xo;
-      const double pxt = sm.xrhs[c] - sigma * xta - ((sm.BD[c][0] * xt[0] + sm.BD[c][1] * xt[1]) + sm.BD[c][2] * xt[2]);
-      pxo = sm.px[c];
-      pxn = alpha * pxt + (1.0 - alpha) * pxo;
-      sm.x[c] = xn;
-      sm.px[c] = pxn;
+      const double xa = sel3(a, xt0, xt1, xt2);
+      const double xn = alpha * xa + (1.0 - alpha) * x;
+      dxv = xn - x;
+      const double pxt = xr - sigma * xa - kd;
+      pxo = px;
+      px = alpha * pxt + (1.0 - alpha) * px;
+      x = xn;
     }
-    // gather helper: var lane a sums A~'v over its foot's rows from the row lanes' (am v, az v)
-    //   fx: am0 v0 + am1 v1;  fy: am2 v2 + am3 v3;  fz: az0 v0 + az1 v1 + az2 v2 + az3 v3 + am4 v4
-    const int gbase = t & ~15;
-    auto gather = [&](double cm, double cz, double init) {
-      const int s0 = gbase + (a == 1 ? 2 : 0), s1 = gbase + (a == 1 ? 3 : 1);
-      const double m0 = __shfl(cm, s0), m1 = __shfl(cm, s1);
-      const double z0 = __shfl(cz, gbase + 0), z1 = __shfl(cz, gbase + 1);
-      const double z2 = __shfl(cz, gbase + 2), z3 = __shfl(cz, gbase + 3);
-      const double m4 = __shfl(cm, gbase + 4);
-      if (a == 2) return ((((init + z0) + z1) + z2) + z3) + m4;
-      return (init + m0) + m1;
-    };
 
     if (need_info) {
       // ---- update_info / check_termination / adapt_rho (osqp.c, auxil.c) ----
-      // row lanes need the new x of their foot; var lanes A~'y of the new y
-      const double x0n = __shfl(xn, gbase + 5), x1n = __shfl(xn, gbase + 6), x2n = __shfl(xn, gbase + 7);
-      double ax = 0.0;
-      if (row_lane) ax = tc < 4 ? am * (tc < 2 ? x0n : x1n) + az * x2n : am * x2n;
-      const double aty = gather(am * yn, az * yn, 0.0);
+      // row lanes need the new x of their foot, variable lanes A~'y of the new y
+      const double x0n = __shfl(x, gb + 5), x1n = __shfl(x, gb + 6), x2n = __shfl(x, gb + 7);
+      const double ax = row_lane ? (k0 * x0n + k1 * x1n) + k2 * x2n : 0.0;
+      const double atyg = gather_atv(row_lane ? km * y : 0.0, row_lane ? kz * y : 0.0, a, 0.0);
+      const double aty = var_lane ? atyg : 0.0;
+      double pr = 0.0, d = 0.0;
+      if (row_lane) pr = ax + (-1.0) * z;
+      if (var_lane) d = (q + 1.0 * px) + 1.0 * aty;
       // the 14 norms of update_info / compute_pri_tol / compute_dua_tol / compute_rho_estimate,
       // reduced one at a time straight into LDS (keeps register pressure flat)
-      double pr = 0.0, ei = 0.0, d = 0.0, di = 0.0, q = 0.0;
-      if (row_lane) {
-        pr = ax + (-1.0) * zn;
-        ei = sm.Einv[r];
-      }
-      if (var_lane) {
-        di = sm.Dinv[c];
-        q = sm.qt[c];
-        d = (q + 1.0 * pxn) + 1.0 * aty;
-      }
       {
         const int lane = t & 63, wave = t >> 6;
         auto put = [&](int k, double v) {
@@ -784,20 +863,20 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
           if (lane == 0) sm.info[wave][k] = v;
           __builtin_amdgcn_sched_barrier(0);
         };
-        put(0, row_lane ? dabs(ei * pr) : 0.0);
+        put(0, row_lane ? dabs(Ei * pr) : 0.0);
         put(1, row_lane ? dabs(pr) : 0.0);
-        put(2, row_lane ? dabs(ei * zn) : 0.0);
-        put(3, row_lane ? dabs(zn) : 0.0);
-        put(4, row_lane ? dabs(ei * ax) : 0.0);
+        put(2, row_lane ? dabs(Ei * z) : 0.0);
+        put(3, row_lane ? dabs(z) : 0.0);
+        put(4, row_lane ? dabs(Ei * ax) : 0.0);
         put(5, row_lane ? dabs(ax) : 0.0);
-        put(6, var_lane ? dabs(di * d) : 0.0);
+        put(6, var_lane ? dabs(Di * d) : 0.0);
         put(7, var_lane ? dabs(d) : 0.0);
-        put(8, var_lane ? dabs(di * q) : 0.0);
+        put(8, var_lane ? dabs(Di * q) : 0.0);
         put(9, var_lane ? dabs(q) : 0.0);
-        put(10, var_lane ? dabs(di * aty) : 0.0);
+        put(10, var_lane ? dabs(Di * aty) : 0.0);
         put(11, var_lane ? dabs(aty) : 0.0);
-        put(12, var_lane ? dabs(di * pxn) : 0.0);
-        put(13, var_lane ? dabs(pxn) : 0.0);
+        put(12, var_lane ? dabs(Di * px) : 0.0);
+        put(13, var_lane ? dabs(px) : 0.0);
       }
       __syncthreads();
       // workgroup maxima read from LDS where they are used (not held across the check)
@@ -820,22 +899,22 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
         if (!prim_ok) {
           // is_primal_infeasible: project delta_y onto the polar of the recession cone (in place)
           if (row_lane) {
-            if (sm.hi[r] > OSQP_INF * MIN_SCALING) {
-              if (sm.lo[r] < -OSQP_INF * MIN_SCALING) dyv = 0.0;
+            if (hi > OSQP_INF * MIN_SCALING) {
+              if (lo < -OSQP_INF * MIN_SCALING) dyv = 0.0;
               else dyv = dmin(dyv, 0.0);
-            } else if (sm.lo[r] < -OSQP_INF * MIN_SCALING) {
+            } else if (lo < -OSQP_INF * MIN_SCALING) {
               dyv = dmax(dyv, 0.0);
             }
           }
-          double nd[1] = {row_lane ? dabs(sm.E[r] * dyv) : 0.0};
+          double nd[1] = {row_lane ? dabs(E * dyv) : 0.0};
           wg_reduce<N, 1, true>(sm, nd, rslot);
           const double ndy = nd[0];
           if (ndy > DIV_TOL) {
-            double lh[1] = {row_lane ? sm.hi[r] * dmax(dyv, 0.0) + sm.lo[r] * dmin(dyv, 0.0) : 0.0};
+            double lh[1] = {row_lane ? hi * dmax(dyv, 0.0) + lo * dmin(dyv, 0.0) : 0.0};
             wg_reduce<N, 1, false>(sm, lh, rslot);
             if (lh[0] < eps_pinf * ndy) {
-              const double atd = gather(am * dyv, az * dyv, 0.0);
-              double an[1] = {var_lane ? dabs(sm.Dinv[c] * atd) : 0.0};
+              const double atd = gather_atv(row_lane ? km * dyv : 0.0, row_lane ? kz * dyv : 0.0, a, 0.0);
+              double an[1] = {var_lane ? dabs(Di * atd) : 0.0};
               wg_reduce<N, 1, true>(sm, an, rslot);
               prim_inf = an[0] < eps_pinf * ndy;
             }
@@ -845,23 +924,22 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
         const bool dual_ok = dua_res < eps_dual;
         if (!dual_ok) {
           // is_dual_infeasible (P~ delta_x = P~x_new - P~x_old)
-          double nx[1] = {var_lane ? dabs(sm.D[c] * dxv) : 0.0};
+          double nx[1] = {var_lane ? dabs(D * dxv) : 0.0};
           wg_reduce<N, 1, true>(sm, nx, rslot);
           const double ndx = nx[0];
           if (ndx > DIV_TOL) {
             double qd[1] = {var_lane ? q * dxv : 0.0};
             wg_reduce<N, 1, false>(sm, qd, rslot);
             if (qd[0] < cost_c * eps_dinf * ndx) {
-              double pd[1] = {var_lane ? dabs(sm.Dinv[c] * (pxn - pxo)) : 0.0};
+              double pd[1] = {var_lane ? dabs(Di * (px - pxo)) : 0.0};
               wg_reduce<N, 1, true>(sm, pd, rslot);
               if (pd[0] < cost_c * eps_dinf * ndx) {
-                const double dx0 = __shfl(dxv, gbase + 5), dx1 = __shfl(dxv, gbase + 6), dx2 = __shfl(dxv, gbase + 7);
+                const double dx0 = __shfl(dxv, gb + 5), dx1 = __shfl(dxv, gb + 6), dx2 = __shfl(dxv, gb + 7);
                 double viol = 0.0;
                 if (row_lane) {
-                  const double adx = tc < 4 ? am * (tc < 2 ? dx0 : dx1) + az * dx2 : am * dx2;
-                  const double v = sm.Einv[r] * adx;
-                  if ((sm.hi[r] < OSQP_INF * MIN_SCALING && v > eps_dinf * ndx) ||
-                      (sm.lo[r] > -OSQP_INF * MIN_SCALING && v < -eps_dinf * ndx))
+                  const double v = Ei * ((k0 * dx0 + k1 * dx1) + k2 * dx2);
+                  if ((hi < OSQP_INF * MIN_SCALING && v > eps_dinf * ndx) ||
+                      (lo > -OSQP_INF * MIN_SCALING && v < -eps_dinf * ndx))
                     viol = 1.0;
                 }
                 double vv[1] = {viol};
@@ -901,38 +979,53 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
       if (last && st == MPCQP_STATUS_UNSOLVED) st = MPCQP_STATUS_MAX_ITER_REACHED;
       if (last) done = true;
       status = st;
+#ifdef MPCQP_PHASE_TIMING
+      if (is_check) PHASE_MARK(30);
+#else
       if (trace && t == 0 && inst < trace_cap && ntrace < MPCQP_TRACE_LEN && is_check) {
         double* tp = trace + ((size_t)inst * MPCQP_TRACE_LEN + ntrace) * 4;
         tp[0] = iter; tp[1] = pri_res; tp[2] = dua_res; tp[3] = rho;
       }
+#endif
       ntrace += is_check ? 1 : 0;
       if (done) break;
       if (refactor) {
         // osqp_update_rho: new rho vector and A~'rho A~ blocks now; P~ reload + re-inversion at
         // the top of the next iteration
-        if (row_lane) set_row_rho<N>(sm, r, rho, false);
-        if (var_lane) compute_bd_row<N>(sm, f, a);
+        if (row_lane) {
+          rho_r = ct == -1 ? rho_r : ct == 1 ? RHO_EQ_OVER_RHO_INEQ * rho : rho;
+          rinv = 1. / rho_r;
+          sm.rowc[5 * f + tc][3] = rho_r;
+        }
+        wave_sync();
+        if (var_lane) {
+          bd_row<N>(sm, f, a, k0, k1, k2);
+          sm.BD[c][0] = k0;
+          sm.BD[c][1] = k1;
+          sm.BD[c][2] = k2;
+        }
         need_factor = true;
       }
     }
     // (a) next right-hand side: rhs = sigma x - q~ + A~'(rho z - y)  [compute_rhs + KKT rhs]
     {
-      double tv = 0.0;
+      double mv = 0.0, zv = 0.0, init = 0.0;
       if (row_lane) {
-        am = sm.am[r];
-        az = sm.az[r];
-        tv = sm.rho_v[r] * sm.z[r] - sm.y[r];
+        const double tv = rho_r * z - y;
+        mv = km * tv;
+        zv = kz * tv;
       }
-      const double init = var_lane ? sigma * sm.x[c] - sm.qt[c] : 0.0;
-      const double rr = gather(am * tv, az * tv, init);
+      if (var_lane) init = sigma * x - q;
+      const double rr = gather_atv(mv, zv, a, init);
       if (var_lane) {
-        sm.rhs[(iter + 1) & 1][c] = rr;  // other buffer: slower waves may still read this one
-        sm.xrhs[c] = rr;
+        xr = rr;
+        sm.rhs[(iter + 1) & 1][c] = xr;  // other buffer: slower waves may still read this one
       }
     }
     __syncthreads();
   }
 
+  PHASE_MARK(20);
   // ---- 4. store_solution + unscale + compute_grf extraction (A1RobotControl.cpp:555-561) ------
   const bool has_sol = status != MPCQP_STATUS_PRIMAL_INFEASIBLE &&
                        status != MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE &&
@@ -940,14 +1033,14 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
                        status != MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE && status != MPCQP_STATUS_NON_CVX;
   {
     // objective 1/2 x'P~x + q~'x (unscaled by cinv)
-    double ob[1] = {var_lane ? 0.5 * sm.x[c] * sm.px[c] + sm.qt[c] * sm.x[c] : 0.0};
+    double ob[1] = {var_lane ? 0.5 * x * px + q * x : 0.0};
     wg_reduce<N, 1, false>(sm, ob, rslot);
-    const double xs = has_sol ? sm.D[c] * sm.x[c] : NAN;
+    const double xs = has_sol ? D * x : NAN;
     if (solution && var_lane) solution[(size_t)inst * n + c] = xs;
     if (f < 4) {  // horizon step 0 = feet 0..3 = legs FL, FR, RL, RR
       mpcqp_result* res = results + inst;
-      const int gbase = t0 & ~15;
-      const double u0 = __shfl(xs, gbase + 5), u1 = __shfl(xs, gbase + 6), u2 = __shfl(xs, gbase + 7);
+      const int gb = t0 & ~7;
+      const double u0 = __shfl(xs, gb + 5), u1 = __shfl(xs, gb + 6), u2 = __shfl(xs, gb + 7);
       const double nrm = sqrt(u0 * u0 + u1 * u1 + u2 * u2);
       const bool nanleg = isnan(nrm);
       if (var_lane) {
@@ -962,7 +1055,7 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
       const unsigned long long nb = __ballot(nanleg && tc == 0);
       if (t0 == 0) {
         int legs = 0;
-        for (int l = 0; l < 4; ++l) legs |= ((nb >> (16 * l)) & 1ull) ? (1 << l) : 0;
+        for (int l = 0; l < 4; ++l) legs |= ((nb >> (8 * l)) & 1ull) ? (1 << l) : 0;
         res->nan_legs = legs;
         double obj;
         if (has_sol) obj = ob[0] * cinv;
@@ -1051,10 +1144,10 @@ hipError_t occupancy_any(int horizon, int* blocks) {
     default: return hipErrorInvalidValue;
   }
 }
-int solve_threads(int horizon) { return 16 * 4 * horizon; }
-size_t workspace_doubles(int horizon) {
+int solve_threads(int horizon) { return ((8 * 4 * horizon + 63) / 64) * 64; }
+size_t workspace_doubles(int horizon) {  // n x NP per robot (Dim<N>::NP = 8 * 3 * ceil(n / 24))
   const int n = 12 * horizon;
-  return (size_t)n * 16 * ((n + 15) / 16);
+  return (size_t)n * 8 * 3 * ((n + 23) / 24);
 }
 
 }  // namespace mpcqp

@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libmpcqp.so")
+# MPCQP_LIB overrides the in-tree library (A/B kernel experiments only).
+LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(PKG_ROOT, "lib", "libmpcqp.so")
 
 STATE_DIM, NUM_LEG, NUM_DOF, CONSTRAINT_DIM = 13, 4, 12, 20
 MAX_HORIZON = 10

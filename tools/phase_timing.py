@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""In-kernel phase timing: run a library built with -DMPCQP_PHASE_TIMING
+(`make -C go1-qp-mpc-controller_amd variant OUT=../abtest/timing.so DEFS=-DMPCQP_PHASE_TIMING`,
+selected with MPCQP_LIB) and report median shader-clock cycles per phase over the traced robots.
+
+Marks: 0 start, 1 record loaded, 2 condensed, 3 Ruiz done, 10/11/12 factorization
+(before load / after load / after inversion), 30 termination checks, 20 loop exit.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "go1-qp-mpc-controller_amd"))
+import mpcqp  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--traced", type=int, default=512)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    st = mpcqp.synthetic_go1(a.batch, seed=1000, gait="trot")
+    recs = mpcqp.assemble_compute_grf(st, 10)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+        d_rec = torch.from_numpy(recs).cuda()
+        d_res = torch.zeros((a.batch, mpcqp._lib.RESULT_DOUBLES), dtype=torch.float64, device="cuda")
+        tr = torch.full((a.traced, 64, 4), float("nan"), dtype=torch.float64, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        for _ in range(2):
+            tr.fill_(float("nan"))
+            s.solve_device_trace(d_rec.data_ptr(), a.batch, d_res.data_ptr(), 0, tr.data_ptr(), a.traced, stream)
+        torch.cuda.synchronize()
+        marks = tr.cpu().numpy().reshape(a.traced, 128, 2)
+        res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
+    phases = {"load": [], "condense": [], "ruiz": [], "tile_reload": [], "invert": [], "first_to_exit": [],
+              "total": [], "iter_cycles": []}
+    for b in range(a.traced):
+        mk = marks[b]
+        mk = mk[~np.isnan(mk[:, 0])]
+        ids, cyc = mk[:, 0].astype(int), mk[:, 1]
+        at = {}
+        for i, c in zip(ids, cyc):
+            at.setdefault(i, []).append(c)
+        phases["load"].append(at[1][0] - at[0][0])
+        phases["condense"].append(at[2][0] - at[1][0])
+        phases["ruiz"].append(at[3][0] - at[2][0])
+        for k in range(len(at[10])):
+            phases["tile_reload"].append(at[11][k] - at[10][k])
+            phases["invert"].append(at[12][k] - at[11][k])
+        phases["total"].append(at[20][0] - at[0][0])
+        inv_total = sum(at[12][k] - at[10][k] for k in range(len(at[10])))
+        loop = at[20][0] - at[12][0] + (at[12][0] - at[10][0]) - inv_total
+        phases["iter_cycles"].append(loop / max(int(res["iters"][b]), 1))
+    out = {k: float(np.median(v)) for k, v in phases.items() if v}
+    out["mean_iters"] = float(res["iters"][: a.traced].mean())
+    out["factorizations_per_robot"] = len(phases["invert"]) / a.traced
+    print(json.dumps(out, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
