@@ -186,7 +186,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS,
                          "traffic": traffic,
-                         "kernel": "mpcqp::solve_kernel<10,4>", "kernel_ms": kern_ms,
+                         "kernel": f"mpcqp::solve_kernel<{N}>", "kernel_ms": kern_ms,
                          "algorithmic_flop_per_launch": flops,
                          "note": "binary64 VALU-bound; peak = FP64 vector (=FP64 MFMA) spec"},
             "cpu_baseline": cpu,

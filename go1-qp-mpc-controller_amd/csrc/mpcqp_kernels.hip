@@ -65,6 +65,7 @@ struct Smem {
   alignas(16) double Dt[Dm::NP];      // Ruiz D_temp
   double red[2][Dm::NW][16];          // workgroup reductions (double-buffered)
   double info[Dm::NW][16];            // per-wave maxima of the termination / rho norms
+  double cst[4];                      // {cost scaling c, rho, pri_res, dua_res}
   union U {
     struct C {
       double S[N][SD * SD];
@@ -443,14 +444,17 @@ __device__ __forceinline__ double gather_atv(double mv, double zv, int a, double
 }
 
 // K = P~ + sigma I + blockdiag(A~' rho A~) from the tile holding P~, then K^-1 in place by block
-// Gauss-Jordan with the 3x3 diagonal block of foot kf as pivot:
+// Gauss-Jordan with the 3x3 diagonal block P of foot kf as pivot.  With R = the raw pivot rows
+// A_k. and W_i = A_ik P^-1 (W_k = I - P^-1 for the pivot rows themselves) every group applies
+// the same update  A_i. <- A_i. - W_i R,  then the pivot columns are set to -W_i (P^-1 for the
+// pivot rows):
 //   A_kk <- P^-1,  A_kj <- P^-1 A_kj,  A_ik <- -A_ik P^-1,  A_ij <- A_ij - A_ik P^-1 A_kj.
 // Pivot kf's columns 3kf..3kf+2 are tile columns 3s..3s+2 of lane L = kf / SPL (s = kf % SPL);
 // unrolling s makes them static register positions.
 template <int N>
 __device__ __forceinline__ void factor_and_invert(double (&M)[3][Dim<N>::BC], Smem<N>& sm, double sigma) {
   using Dm = Dim<N>;
-  constexpr int BC = Dm::BC, n = Dm::n, SPL = Dm::SPL;
+  constexpr int BC = Dm::BC, n = Dm::n, SPL = Dm::SPL, NP = Dm::NP;
   const int t = opaque(threadIdx.x);
   const int f = t >> 3, tc = t & 7;
 #pragma unroll
@@ -459,12 +463,11 @@ __device__ __forceinline__ void factor_and_invert(double (&M)[3][Dim<N>::BC], Sm
 #pragma unroll
     for (int j = 0; j < BC; ++j) {
       const int c = tc * BC + j;
-      if (r < n && c < n) {
-        double v = M[i][j];
-        if (r == c) v += sigma;
-        if (c / 3 == f) v += sm.BD[r][c - 3 * f];
-        M[i][j] = v;
-      }
+      double v = M[i][j];
+      if (r == c && r < n) v += sigma;
+      const int d = c - 3 * f;
+      if (r < n && d >= 0 && d < 3) v += sm.BD[r][d];
+      M[i][j] = v;
     }
   }
   for (int L = 0; L < (Dm::nf + SPL - 1) / SPL; ++L) {
@@ -473,78 +476,63 @@ __device__ __forceinline__ void factor_and_invert(double (&M)[3][Dim<N>::BC], Sm
       const int kf = L * SPL + s;
       if (kf >= Dm::nf) break;
       const int b = kf & 1;
-      const bool piv = f == kf;   // this group owns the pivot rows
-      const bool pl = tc == L;    // this lane holds the pivot columns
-      // ---- phase A: pivot columns of every group, P^-1, and P^-1 A_k. ----
+      const bool own = f == kf;  // this group owns the pivot rows
+      const bool pl = tc == L;   // this lane holds the pivot columns
+      double* __restrict__ Rb = &sm.u.g.r[b][0][tc * BC];
+      // ---- phase A: publish every group's pivot-column block, the raw pivot rows and P^-1 ----
       if (pl) {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int q = 0; q < 3; ++q) sm.u.g.ck[b][f][3 * i + q] = M[i][3 * s + q];
-        if (piv) {
-          double P[9];
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int q = 0; q < 3; ++q) P[3 * i + q] = M[i][3 * s + q];
-          auto cof = [&](int i, int j) {
-            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-            return P[i1 * 3 + j1] * P[i2 * 3 + j2] - P[i1 * 3 + j2] * P[i2 * 3 + j1];
-          };
-          const double det = (cof(0, 0) * P[0] + cof(1, 0) * P[3]) + cof(2, 0) * P[6];
-          const double invdet = 1.0 / det;
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) sm.u.g.pinv[b][j * 3 + i] = cof(i, j) * invdet;
-        }
       }
-      if (piv) {
-        wave_sync();
-        double Pi[9];
+      if (own) {  // raw pivot rows, pivot columns zeroed (those are set explicitly below)
 #pragma unroll
-        for (int e = 0; e < 9; ++e) Pi[e] = sm.u.g.pinv[b][e];
+        for (int j = 0; j < BC; ++j)
 #pragma unroll
-        for (int j = 0; j < BC; ++j) {
-          const double r0 = M[0][j], r1 = M[1][j], r2 = M[2][j];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const double v = (Pi[i * 3] * r0 + Pi[i * 3 + 1] * r1) + Pi[i * 3 + 2] * r2;
-            sm.u.g.r[b][i][tc * BC + j] = v;
-            M[i][j] = v;
-          }
-        }
+          for (int i = 0; i < 3; ++i) Rb[i * NP + j] = (pl && j >= 3 * s && j < 3 * s + 3) ? 0.0 : M[i][j];
         if (pl) {
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int q = 0; q < 3; ++q) M[i][3 * s + q] = Pi[i * 3 + q];
+          const double P0 = M[0][3 * s], P1 = M[0][3 * s + 1], P2 = M[0][3 * s + 2];
+          const double P3 = M[1][3 * s], P4 = M[1][3 * s + 1], P5 = M[1][3 * s + 2];
+          const double P6 = M[2][3 * s], P7 = M[2][3 * s + 1], P8 = M[2][3 * s + 2];
+          // cofactor inverse (Eigen's 3x3 formula)
+          const double c00 = P4 * P8 - P5 * P7, c01 = P5 * P6 - P3 * P8, c02 = P3 * P7 - P4 * P6;
+          const double c10 = P7 * P2 - P8 * P1, c11 = P8 * P0 - P6 * P2, c12 = P6 * P1 - P7 * P0;
+          const double c20 = P1 * P5 - P2 * P4, c21 = P2 * P3 - P0 * P5, c22 = P0 * P4 - P1 * P3;
+          const double invdet = 1.0 / ((c00 * P0 + c10 * P3) + c20 * P6);
+          double* pv = sm.u.g.pinv[b];
+          pv[0] = c00 * invdet; pv[1] = c10 * invdet; pv[2] = c20 * invdet;
+          pv[3] = c01 * invdet; pv[4] = c11 * invdet; pv[5] = c21 * invdet;
+          pv[6] = c02 * invdet; pv[7] = c12 * invdet; pv[8] = c22 * invdet;
         }
       }
       __syncthreads();
-      // ---- phase B: rank-3 update of every other group's rows ----
-      if (!piv) {
-        double Ck[9];
+      // ---- phase B: A_i. -= W_i R for every group, then the pivot columns ----
+      double Pv[9], W[9];
 #pragma unroll
-        for (int e = 0; e < 9; ++e) Ck[e] = sm.u.g.ck[b][f][e];
+      for (int e = 0; e < 9; ++e) Pv[e] = sm.u.g.pinv[b][e];
 #pragma unroll
-        for (int j = 0; j < BC; ++j) {
-          const int c = tc * BC + j;
-          const double R0 = sm.u.g.r[b][0][c], R1 = sm.u.g.r[b][1][c], R2 = sm.u.g.r[b][2][c];
+      for (int i = 0; i < 3; ++i) {
+        const double C0 = sm.u.g.ck[b][f][3 * i], C1 = sm.u.g.ck[b][f][3 * i + 1], C2 = sm.u.g.ck[b][f][3 * i + 2];
 #pragma unroll
-          for (int i = 0; i < 3; ++i)
-            M[i][j] = M[i][j] - ((Ck[i * 3] * R0 + Ck[i * 3 + 1] * R1) + Ck[i * 3 + 2] * R2);
+        for (int q = 0; q < 3; ++q) {
+          const double w = (C0 * Pv[q] + C1 * Pv[3 + q]) + C2 * Pv[6 + q];
+          W[3 * i + q] = own ? (i == q ? 1.0 : 0.0) - Pv[3 * i + q] : w;
         }
-        double Pv[9];
+      }
 #pragma unroll
-        for (int e = 0; e < 9; ++e) Pv[e] = sm.u.g.pinv[b][e];
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const double v = own ? Pv[3 * i + q] : -W[3 * i + q];
+          M[i][3 * s + q] = pl ? v : M[i][3 * s + q];
+        }
+#pragma unroll
+      for (int j = 0; j < BC; ++j) {
+        const double R0 = Rb[j], R1 = Rb[NP + j], R2 = Rb[2 * NP + j];
 #pragma unroll
         for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            const double w = -((Ck[i * 3] * Pv[q] + Ck[i * 3 + 1] * Pv[3 + q]) + Ck[i * 3 + 2] * Pv[6 + q]);
-            M[i][3 * s + q] = pl ? w : M[i][3 * s + q];
-          }
+          M[i][j] = fma(-W[3 * i + 2], R2, fma(-W[3 * i + 1], R1, fma(-W[3 * i], R0, M[i][j])));
       }
     }
   }
@@ -552,13 +540,16 @@ __device__ __forceinline__ void factor_and_invert(double (&M)[3][Dim<N>::BC], Sm
 }
 
 // Phase timing (debug builds with -DMPCQP_PHASE_TIMING): thread 0 of each traced robot appends
-// {phase id, s_memtime} pairs to the trace buffer instead of termination-check records.
+// {phase id, s_memtime, s_memrealtime (100 MHz), 0} records to the trace buffer instead of
+// termination-check records.
 #ifdef MPCQP_PHASE_TIMING
 #define PHASE_MARK(id)                                                                     \
   do {                                                                                     \
-    if (trace && threadIdx.x == 0 && inst < trace_cap && nmark < MPCQP_TRACE_LEN * 2) {    \
-      trace[(size_t)inst * MPCQP_TRACE_LEN * 4 + 2 * nmark] = (id);                        \
-      trace[(size_t)inst * MPCQP_TRACE_LEN * 4 + 2 * nmark + 1] = (double)__builtin_readcyclecounter(); \
+    if (trace && threadIdx.x == 0 && inst < trace_cap && nmark < MPCQP_TRACE_LEN) {        \
+      double* tm_ = trace + ((size_t)inst * MPCQP_TRACE_LEN + nmark) * 4;                   \
+      tm_[0] = (id);                                                                       \
+      tm_[1] = (double)__builtin_readcyclecounter();                                       \
+      tm_[2] = (double)__builtin_amdgcn_s_memrealtime();                                   \
       ++nmark;                                                                             \
     }                                                                                      \
   } while (0)
@@ -567,6 +558,14 @@ __device__ __forceinline__ void factor_and_invert(double (&M)[3][Dim<N>::BC], Sm
   do {                 \
   } while (0)
 #endif
+
+// Per-robot workspace (doubles): the scaled P~ (n x NP, re-read at every rho refactorization),
+// then 12 doubles per thread where a lane parks its ADMM state while the block inverts.
+template <int N>
+struct WS {
+  static constexpr size_t PARK = (size_t)Dim<N>::n * Dim<N>::NP;
+  static constexpr size_t SIZE = PARK + (size_t)12 * Dim<N>::NT;
+};
 
 // ---- the solver kernel ---------------------------------------------------------------------
 template <int N>
@@ -580,7 +579,7 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
   const int inst = blockIdx.x;
   if (inst >= batch) return;
   const int t0 = threadIdx.x;
-  double* __restrict__ Pw = work + (size_t)inst * n * Dm::NP;
+  double* __restrict__ Pw = work + (size_t)inst * WS<N>::SIZE;
   const double alpha = p.alpha, sigma = p.sigma;
   double M[3][BC];
   int rslot = 0;
@@ -725,7 +724,6 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
     if (var_lane) q *= c_temp;
     cost_c *= c_temp;
   }
-  const double cinv = 1. / cost_c;
   if (var_lane) Di = 1. / D;
   if (row_lane) {
     Ei = 1. / E;
@@ -734,7 +732,15 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
   }
   PHASE_MARK(3);
   store_tile<N>(M, Pw, f, tc);  // scaled P~ kept for rho refactorizations
-  double rho = dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
+  // Uniform doubles used only at termination checks live in LDS, not in registers across the
+  // loop: cst = {cost scaling c, rho, pri_res, dua_res}.
+  if (t0 == 0) {
+    sm.cst[0] = cost_c;
+    sm.cst[1] = dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
+    sm.cst[2] = 0.0;
+    sm.cst[3] = 0.0;
+  }
+  const double rho0 = dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
   if (row_lane) {  // set_rho_vec (auxil.c)
     if (lo < -OSQP_INF * MIN_SCALING && hi > OSQP_INF * MIN_SCALING)
       ct = -1;
@@ -742,7 +748,7 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
       ct = 1;
     else
       ct = 0;
-    rho_r = ct == -1 ? RHO_MIN : ct == 1 ? RHO_EQ_OVER_RHO_INEQ * rho : rho;
+    rho_r = ct == -1 ? RHO_MIN : ct == 1 ? RHO_EQ_OVER_RHO_INEQ * rho0 : rho0;
     rinv = 1. / rho_r;
     sm.rowc[r][0] = k0;
     sm.rowc[r][1] = k1;
@@ -761,9 +767,15 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
     px = 0.0;
   }
 
+  // Cold per-lane values (Ruiz factors and their inverses, constraint type) are parked in the
+  // workspace for the whole solve; only the termination checks and the epilogue read them.
+  double* __restrict__ const park0 = Pw + WS<N>::PARK + (size_t)t0 * 12;
+  park0[6] = s_g;
+  park0[7] = s_h;
+  park0[11] = ct;
+
   // ---- 3. ADMM -------------------------------------------------------------------------------
   int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
-  double pri_res = 0.0, dua_res = 0.0;
   // iteration-1 right-hand side from the cold start (x = z = y = 0)
   for (int e = n + t0; e < Dm::NP; e += NT) sm.rhs[0][e] = sm.rhs[1][e] = 0.0;  // padding
   if (var_lane) {
@@ -781,11 +793,19 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
     const int a = tc - 5, c = 3 * f + (a < 0 ? 0 : a);
     const int gb = t & ~7;
     if (need_factor) {  // single inlined site: initial factorization and osqp_update_rho refactors
+      // park the lane's ADMM state in the workspace so the inversion has the register file
+      double* __restrict__ park = Pw + WS<N>::PARK + (size_t)t * 12;
+      park[0] = s_a; park[1] = s_b; park[2] = s_c; park[3] = s_d; park[4] = s_e; park[5] = s_f;
+      park[8] = k0; park[9] = k1; park[10] = k2;
+      asm volatile("" ::: "memory");
       PHASE_MARK(10);
       if (iter > 1) load_tile<N>(M, Pw, f, tc);
       PHASE_MARK(11);
       factor_and_invert<N>(M, sm, sigma);
       PHASE_MARK(12);
+      asm volatile("" ::: "memory");
+      s_a = park[0]; s_b = park[1]; s_c = park[2]; s_d = park[3]; s_e = park[4]; s_f = park[5];
+      k0 = park[8]; k1 = park[9]; k2 = park[10];
       need_factor = false;
     }
     // (b) x~ = K^-1 rhs: register-tile mat-vec, all-reduced inside the foot's 8-lane group
@@ -846,6 +866,9 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
 
     if (need_info) {
       // ---- update_info / check_termination / adapt_rho (osqp.c, auxil.c) ----
+      const double* __restrict__ parkc = Pw + WS<N>::PARK + (size_t)t * 12;
+      const double E = parkc[6], Ei = parkc[7];  // row lanes: E, 1/E; variable lanes: D, 1/D
+      const double &D = E, &Di = Ei;
       // row lanes need the new x of their foot, variable lanes A~'y of the new y
       const double x0n = __shfl(x, gb + 5), x1n = __shfl(x, gb + 6), x2n = __shfl(x, gb + 7);
       const double ax = row_lane ? (k0 * x0n + k1 * x1n) + k2 * x2n : 0.0;
@@ -885,8 +908,10 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
         for (int w = 1; w < Dm::NW; ++w) v = dmax(v, sm.info[w][k]);
         return v;
       };
-      pri_res = mx(0);
-      dua_res = cinv * mx(6);
+      const double cost_c = sm.cst[0], cinv = 1. / cost_c;
+      double rho = sm.cst[1];
+      const double pri_res = mx(0);
+      const double dua_res = cinv * mx(6);
       iters = iter;
       // check_termination (osqp.c): approx=1 is the post-loop check at max_iter (eps x 10)
       auto check = [&](bool approx) -> int {
@@ -988,11 +1013,17 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
       }
 #endif
       ntrace += is_check ? 1 : 0;
+      if (t == 0) {  // every thread holds the same values; the reads above precede a barrier
+        sm.cst[1] = rho;
+        sm.cst[2] = pri_res;
+        sm.cst[3] = dua_res;
+      }
       if (done) break;
       if (refactor) {
         // osqp_update_rho: new rho vector and A~'rho A~ blocks now; P~ reload + re-inversion at
         // the top of the next iteration
         if (row_lane) {
+          const int ct = (int)parkc[11];
           rho_r = ct == -1 ? rho_r : ct == 1 ? RHO_EQ_OVER_RHO_INEQ * rho : rho;
           rinv = 1. / rho_r;
           sm.rowc[5 * f + tc][3] = rho_r;
@@ -1027,6 +1058,8 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
 
   PHASE_MARK(20);
   // ---- 4. store_solution + unscale + compute_grf extraction (A1RobotControl.cpp:555-561) ------
+  __syncthreads();
+  const double cinv = 1. / sm.cst[0], rho = sm.cst[1], pri_res = sm.cst[2], dua_res = sm.cst[3];
   const bool has_sol = status != MPCQP_STATUS_PRIMAL_INFEASIBLE &&
                        status != MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE &&
                        status != MPCQP_STATUS_DUAL_INFEASIBLE &&
@@ -1035,7 +1068,7 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
     // objective 1/2 x'P~x + q~'x (unscaled by cinv)
     double ob[1] = {var_lane ? 0.5 * x * px + q * x : 0.0};
     wg_reduce<N, 1, false>(sm, ob, rslot);
-    const double xs = has_sol ? D * x : NAN;
+    const double xs = has_sol ? park0[6] * x : NAN;  // D x
     if (solution && var_lane) solution[(size_t)inst * n + c] = xs;
     if (f < 4) {  // horizon step 0 = feet 0..3 = legs FL, FR, RL, RR
       mpcqp_result* res = results + inst;
@@ -1145,9 +1178,9 @@ hipError_t occupancy_any(int horizon, int* blocks) {
   }
 }
 int solve_threads(int horizon) { return ((8 * 4 * horizon + 63) / 64) * 64; }
-size_t workspace_doubles(int horizon) {  // n x NP per robot (Dim<N>::NP = 8 * 3 * ceil(n / 24))
+size_t workspace_doubles(int horizon) {  // WS<N>::SIZE
   const int n = 12 * horizon;
-  return (size_t)n * 8 * 3 * ((n + 23) / 24);
+  return (size_t)n * 8 * 3 * ((n + 23) / 24) + (size_t)12 * solve_threads(horizon);
 }
 
 }  // namespace mpcqp

@@ -186,3 +186,47 @@ def synthetic_go1(batch, seed=0, gait="trot", mixed_mu=False):
         root_rot_mat=R, root_euler_d=np.zeros((B, 3)),
         root_pos_d=np.stack([np.zeros(B), np.zeros(B), pzd], 1), root_ang_vel_d=wd,
         root_lin_vel_d=vd, foot_pos_abs=feet_abs, contacts=contacts, mu=mu)
+
+
+def synthetic_go1_ticks(batch, ticks, seed=0, gait="trot", period=0.0025, swing_ticks=40):
+    """Seeded closed-loop-like trajectories for warm-start tests: ``ticks`` consecutive control
+    ticks of ``batch`` robots (list of RobotStates, one per tick).
+
+    From synthetic_go1's states, each tick integrates the pose with the current velocities over
+    ``period``, relaxes the velocities toward the command with a small random walk, keeps the
+    body-frame feet fixed, and (gait "trot") switches the FL+RR / FR+RL stance pair every
+    ``swing_ticks`` ticks with a per-robot phase offset; "stance" keeps all four feet down.
+    """
+    base = synthetic_go1(batch, seed=seed, gait="stance")
+    rng = np.random.Generator(np.random.PCG64(seed + 7919))
+    B = batch
+    euler = base.root_euler.copy()
+    pos = base.root_pos.copy()
+    v = base.root_lin_vel.copy()
+    w = base.root_ang_vel.copy()
+    R0 = base.root_rot_mat
+    feet_body = np.einsum("bji,blj->bli", R0, base.foot_pos_abs)  # R^T feet_abs
+    phase0 = rng.integers(0, 2 * swing_ticks, B)
+    out = []
+    for t in range(ticks):
+        R = rot_zyx(euler[:, 0], euler[:, 1], euler[:, 2])
+        feet_abs = np.einsum("bij,blj->bli", R, feet_body)
+        if gait == "trot":
+            ph = (((t + phase0) // swing_ticks) % 2).astype(bool)
+            contacts = np.stack([~ph, ph, ph, ~ph], 1)
+        elif gait == "stance":
+            contacts = np.ones((B, 4), dtype=bool)
+        else:
+            raise ValueError(gait)
+        out.append(RobotStates(
+            root_euler=euler.copy(), root_pos=pos.copy(), root_ang_vel=w.copy(), root_lin_vel=v.copy(),
+            root_rot_mat=R, root_euler_d=base.root_euler_d, root_pos_d=base.root_pos_d,
+            root_ang_vel_d=base.root_ang_vel_d, root_lin_vel_d=base.root_lin_vel_d,
+            foot_pos_abs=feet_abs, contacts=contacts, mu=base.mu))
+        vd_world = np.einsum("bij,bj->bi", R, base.root_lin_vel_d)
+        pos = pos + v * period
+        euler = euler + np.stack([w[:, 0], w[:, 1], w[:, 2]], 1) * period
+        euler[:, :2] = np.clip(euler[:, :2], -0.2, 0.2)
+        v = v + 0.05 * (vd_world - v) + rng.normal(0.0, 0.01, (B, 3))
+        w = w + 0.05 * (base.root_ang_vel_d - w) + rng.normal(0.0, 0.01, (B, 3))
+    return out

@@ -385,6 +385,7 @@ typedef struct {
       *Pdelta_x, *Adelta_x, *D_temp, *D_temp_A, *E_temp;
   /* KKT */
   double *K, *L;
+  double* pool; /* backing store of the vectors above */
   /* settings */
   const mpcqp_params* st;
   /* info */
@@ -948,148 +949,170 @@ static int record_has_nonfinite(const double* rec, int N) {
   return 0;
 }
 
-int32_t orc_solve(const mpcqp_params* prm, const double* rec, mpcqp_result* res, double* sol,
-                  orc_trace_entry* trace, int32_t max_trace, int32_t* n_trace) {
-  const int N = prm->horizon;
-  if (N < 1 || !res) return MPCQP_ERR_INVALID_ARG;
-  const int n = ND * N, m = CD * N;
-  int ntr = 0;
-  memset(res, 0, sizeof(*res));
-  if (n_trace) *n_trace = 0;
-  if (record_has_nonfinite(rec, N)) {
-    res->status = MPCQP_STATUS_NAN_INPUT;
-    res->nan_legs = 0xF;
-    if (sol)
-      for (int i = 0; i < n; ++i) sol[i] = OSQP_NAN;
-    return MPCQP_OK;
-  }
-  double* Pd = (double*)malloc(sizeof(double) * (size_t)n * n);
-  double* Ad = (double*)malloc(sizeof(double) * (size_t)m * n);
-  osqp_ws w;
-  memset(&w, 0, sizeof(w));
-  w.n = n;
-  w.m = m;
-  w.st = prm;
-  w.q = (double*)malloc(sizeof(double) * n);
-  w.l = (double*)malloc(sizeof(double) * m);
-  w.u = (double*)malloc(sizeof(double) * m);
-  orc_build_qp(prm, rec, Pd, w.q, w.l, w.u, Ad);
-  /* OsqpEigen::Data::setHessianMatrix keeps triangularView<Upper> of hessian.sparseView() */
-  w.P = dense_to_csc_upper(Pd, n);
-  w.A = dense_to_csc(Ad, m, n);
-  free(Pd);
-  free(Ad);
-  for (int i = 0; i < m; ++i) { /* osqp_setup clips bounds to +-OSQP_INFTY */
-    w.l[i] = c_max(w.l[i], -OSQP_INFTY);
-    w.u[i] = c_min(w.u[i], OSQP_INFTY);
-  }
+/* ---- workspace lifetime ------------------------------------------------------------------- */
+static void ws_alloc(osqp_ws* w, const mpcqp_params* prm) {
+  const int N = prm->horizon, n = ND * N, m = CD * N;
+  memset(w, 0, sizeof(*w));
+  w->n = n;
+  w->m = m;
+  w->st = prm;
+  w->q = (double*)malloc(sizeof(double) * n);
+  w->l = (double*)malloc(sizeof(double) * m);
+  w->u = (double*)malloc(sizeof(double) * m);
   double* pool = (double*)calloc((size_t)(15 * n + 12 * m + 2 * (n + m)), sizeof(double));
+  w->pool = pool;
   double* pp = pool;
 #define TAKE(ptr, cnt) \
   ptr = pp;            \
   pp += (cnt)
-  TAKE(w.D, n);
-  TAKE(w.Dinv, n);
-  TAKE(w.E, m);
-  TAKE(w.Einv, m);
-  TAKE(w.rho_vec, m);
-  TAKE(w.rho_inv_vec, m);
-  TAKE(w.x, n);
-  TAKE(w.y, m);
-  TAKE(w.z, m);
-  TAKE(w.xz_tilde, n + m);
-  TAKE(w.x_prev, n);
-  TAKE(w.z_prev, m);
-  TAKE(w.Ax, m);
-  TAKE(w.Px, n);
-  TAKE(w.Aty, n);
-  TAKE(w.delta_y, m);
-  TAKE(w.Atdelta_y, n);
-  TAKE(w.delta_x, n);
-  TAKE(w.Pdelta_x, n);
-  TAKE(w.Adelta_x, m);
-  TAKE(w.D_temp, n);
-  TAKE(w.D_temp_A, n);
-  TAKE(w.E_temp, m);
+  TAKE(w->D, n);
+  TAKE(w->Dinv, n);
+  TAKE(w->E, m);
+  TAKE(w->Einv, m);
+  TAKE(w->rho_vec, m);
+  TAKE(w->rho_inv_vec, m);
+  TAKE(w->x, n);
+  TAKE(w->y, m);
+  TAKE(w->z, m);
+  TAKE(w->xz_tilde, n + m);
+  TAKE(w->x_prev, n);
+  TAKE(w->z_prev, m);
+  TAKE(w->Ax, m);
+  TAKE(w->Px, n);
+  TAKE(w->Aty, n);
+  TAKE(w->delta_y, m);
+  TAKE(w->Atdelta_y, n);
+  TAKE(w->delta_x, n);
+  TAKE(w->Pdelta_x, n);
+  TAKE(w->Adelta_x, m);
+  TAKE(w->D_temp, n);
+  TAKE(w->D_temp_A, n);
+  TAKE(w->E_temp, m);
 #undef TAKE
-  w.constr_type = (int*)calloc(m, sizeof(int));
-  w.K = (double*)malloc(sizeof(double) * (size_t)n * n);
-  w.L = (double*)malloc(sizeof(double) * (size_t)n * n);
-  w.rho = prm->rho;
-  w.status = MPCQP_STATUS_UNSOLVED;
+  w->constr_type = (int*)calloc(m, sizeof(int));
+  w->K = (double*)malloc(sizeof(double) * (size_t)n * n);
+  w->L = (double*)malloc(sizeof(double) * (size_t)n * n);
+  w->rho = prm->rho;
+  w->status = MPCQP_STATUS_UNSOLVED;
+}
+static void ws_free(osqp_ws* w) {
+  csc_free(&w->P);
+  csc_free(&w->A);
+  free(w->q);
+  free(w->l);
+  free(w->u);
+  free(w->pool);
+  free(w->constr_type);
+  free(w->K);
+  free(w->L);
+  memset(w, 0, sizeof(*w));
+}
 
-  /* osqp_setup */
-  if (prm->scaling)
-    scale_data(&w);
-  else {
-    w.c = w.cinv = 1.0;
-    vec_set_scalar(w.D, 1., n);
-    vec_set_scalar(w.Dinv, 1., n);
-    vec_set_scalar(w.E, 1., m);
-    vec_set_scalar(w.Einv, 1., m);
+/* osqp_setup on the QP of `rec` (OsqpEigen::Solver::initSolver, A1RobotControl.cpp:521-531):
+ * data copy, bound clipping, scale_data, set_rho_vec, KKT factorization; x = z = y = 0. */
+static int ws_setup(osqp_ws* w, const double* rec) {
+  const int n = w->n, m = w->m;
+  double* Pd = (double*)malloc(sizeof(double) * (size_t)n * n);
+  double* Ad = (double*)malloc(sizeof(double) * (size_t)m * n);
+  orc_build_qp(w->st, rec, Pd, w->q, w->l, w->u, Ad);
+  /* OsqpEigen::Data::setHessianMatrix keeps triangularView<Upper> of hessian.sparseView() */
+  csc_free(&w->P);
+  csc_free(&w->A);
+  w->P = dense_to_csc_upper(Pd, n);
+  w->A = dense_to_csc(Ad, m, n);
+  free(Pd);
+  free(Ad);
+  for (int i = 0; i < m; ++i) { /* osqp_setup clips bounds to +-OSQP_INFTY */
+    w->l[i] = c_max(w->l[i], -OSQP_INFTY);
+    w->u[i] = c_min(w->u[i], OSQP_INFTY);
   }
-  set_rho_vec(&w);
-  int fail = factor_kkt(&w);
+  w->rho = w->st->rho;
+  if (w->st->scaling)
+    scale_data(w);
+  else {
+    w->c = w->cinv = 1.0;
+    vec_set_scalar(w->D, 1., n);
+    vec_set_scalar(w->Dinv, 1., n);
+    vec_set_scalar(w->E, 1., m);
+    vec_set_scalar(w->Einv, 1., m);
+  }
+  set_rho_vec(w);
+  vec_set_scalar(w->x, 0., n);
+  vec_set_scalar(w->z, 0., m);
+  vec_set_scalar(w->y, 0., m);
+  return factor_kkt(w);
+}
 
-  /* osqp_solve (cold start: x = z = y = 0) */
+/* OSQP 0.6 osqp_solve main loop + post-loop checks, from the iterates currently in `w` (zero
+ * after ws_setup = cold start; the previous solution = warm start). */
+static int ws_admm(osqp_ws* w, int fail, orc_trace_entry* trace, int32_t max_trace, int32_t* n_trace) {
+  const mpcqp_params* prm = w->st;
+  int ntr = 0;
   int iter = 0, can_check_termination = 0;
+  w->status = MPCQP_STATUS_UNSOLVED;
+  w->rho_updates = 0; /* reset_info */
   if (!fail) {
     for (iter = 1; iter <= prm->max_iter; iter++) {
       double* t;
-      t = w.x; w.x = w.x_prev; w.x_prev = t; /* swap_vectors */
-      t = w.z; w.z = w.z_prev; w.z_prev = t;
-      update_xz_tilde(&w);
-      update_x(&w);
-      update_z(&w);
-      update_y(&w);
+      t = w->x; w->x = w->x_prev; w->x_prev = t; /* swap_vectors */
+      t = w->z; w->z = w->z_prev; w->z_prev = t;
+      update_xz_tilde(w);
+      update_x(w);
+      update_z(w);
+      update_y(w);
       can_check_termination = prm->check_termination && (iter % prm->check_termination == 0);
       double ep = 0, ed = 0;
       int done = 0;
       if (can_check_termination) {
-        update_info(&w, iter);
-        done = check_termination(&w, 0, &ep, &ed);
+        update_info(w, iter);
+        done = check_termination(w, 0, &ep, &ed);
       }
       int rho_upd = 0;
       if (!done && prm->adaptive_rho && prm->adaptive_rho_interval &&
           (iter % prm->adaptive_rho_interval == 0)) {
-        if (!can_check_termination) update_info(&w, iter);
-        int before = w.rho_updates;
-        if (adapt_rho(&w)) {
+        if (!can_check_termination) update_info(w, iter);
+        int before = w->rho_updates;
+        if (adapt_rho(w)) {
           fail = 1;
         }
-        rho_upd = w.rho_updates != before;
+        rho_upd = w->rho_updates != before;
       }
       if (trace && can_check_termination && ntr < max_trace) {
         orc_trace_entry* e = &trace[ntr++];
         e->iter = iter;
         e->rho_updated = rho_upd;
-        e->pri_res = w.pri_res;
-        e->dua_res = w.dua_res;
+        e->pri_res = w->pri_res;
+        e->dua_res = w->dua_res;
         e->eps_prim = ep;
         e->eps_dual = ed;
-        e->rho = w.rho;
+        e->rho = w->rho;
       }
       if (done || fail) break;
     }
     if (!can_check_termination && !fail) {
-      update_info(&w, iter - 1);
-      check_termination(&w, 0, NULL, NULL);
+      update_info(w, iter - 1);
+      check_termination(w, 0, NULL, NULL);
     }
-    if (w.status == MPCQP_STATUS_UNSOLVED && !fail) {
-      if (!check_termination(&w, 1, NULL, NULL)) w.status = MPCQP_STATUS_MAX_ITER_REACHED;
+    if (w->status == MPCQP_STATUS_UNSOLVED && !fail) {
+      if (!check_termination(w, 1, NULL, NULL)) w->status = MPCQP_STATUS_MAX_ITER_REACHED;
     }
   }
-  if (fail) w.status = MPCQP_STATUS_NON_CVX;
-  if (has_solution(w.status)) w.obj_val = compute_obj_val(&w, w.x);
+  if (fail) w->status = MPCQP_STATUS_NON_CVX;
+  if (has_solution(w->status)) w->obj_val = compute_obj_val(w, w->x);
+  if (n_trace) *n_trace = ntr;
+  return fail;
+}
 
-  /* store_solution + unscale_solution: x = D x */
+/* store_solution + unscale_solution (x = D x) and compute_grf's extraction
+ * (A1RobotControl.cpp:555-561). */
+static void ws_extract(const osqp_ws* w, const double* rec, mpcqp_result* res, double* sol) {
+  const int n = w->n;
   double* xs = (double*)malloc(sizeof(double) * n);
-  if (has_solution(w.status)) {
-    for (int i = 0; i < n; ++i) xs[i] = prm->scaling ? w.D[i] * w.x[i] : w.x[i];
+  if (has_solution(w->status)) {
+    for (int i = 0; i < n; ++i) xs[i] = w->st->scaling ? w->D[i] * w->x[i] : w->x[i];
   } else {
     for (int i = 0; i < n; ++i) xs[i] = OSQP_NAN;
   }
-  /* A1RobotControl.cpp:555-561 */
   const double* R = rec + MPCQP_REC_ROT;
   for (int k = 0; k < ND; ++k) res->u0[k] = xs[k];
   for (int leg = 0; leg < NL; ++leg) {
@@ -1107,25 +1130,226 @@ int32_t orc_solve(const mpcqp_params* prm, const double* rec, mpcqp_result* res,
     }
   }
   if (sol) memcpy(sol, xs, sizeof(double) * n);
-  res->obj_val = w.obj_val;
-  res->pri_res = w.pri_res;
-  res->dua_res = w.dua_res;
-  res->rho = w.rho;
-  res->status = w.status;
-  res->iters = w.iter;
-  res->rho_updates = w.rho_updates;
-  if (n_trace) *n_trace = ntr;
-
+  res->obj_val = w->obj_val;
+  res->pri_res = w->pri_res;
+  res->dua_res = w->dua_res;
+  res->rho = w->rho;
+  res->status = w->status;
+  res->iters = w->iter;
+  res->rho_updates = w->rho_updates;
   free(xs);
-  csc_free(&w.P);
-  csc_free(&w.A);
-  free(w.q);
-  free(w.l);
-  free(w.u);
-  free(pool);
-  free(w.constr_type);
-  free(w.K);
-  free(w.L);
+}
+
+int32_t orc_solve(const mpcqp_params* prm, const double* rec, mpcqp_result* res, double* sol,
+                  orc_trace_entry* trace, int32_t max_trace, int32_t* n_trace) {
+  const int N = prm->horizon;
+  if (N < 1 || !res) return MPCQP_ERR_INVALID_ARG;
+  const int n = ND * N;
+  memset(res, 0, sizeof(*res));
+  if (n_trace) *n_trace = 0;
+  if (record_has_nonfinite(rec, N)) {
+    res->status = MPCQP_STATUS_NAN_INPUT;
+    res->nan_legs = 0xF;
+    if (sol)
+      for (int i = 0; i < n; ++i) sol[i] = OSQP_NAN;
+    return MPCQP_OK;
+  }
+  osqp_ws w;
+  ws_alloc(&w, prm);
+  int fail = ws_setup(&w, rec);
+  ws_admm(&w, fail, trace, max_trace, n_trace);
+  ws_extract(&w, rec, res, sol);
+  ws_free(&w);
+  return MPCQP_OK;
+}
+
+/* ============================================================================================
+ * Warm start across control ticks: the persistent solver of A1RobotControl.h:67 driven as in
+ * A1RobotControl.cpp:520-540 (OsqpEigen 0.6.3 on OSQP 0.6).
+ * ========================================================================================== */
+
+/* OSQP 0.6 unscale_data (scaling.c) */
+static void unscale_data(osqp_ws* w) {
+  const int n = w->n, m = w->m;
+  mat_mult_scalar(&w->P, w->cinv);
+  mat_premult_diag(&w->P, w->Dinv);
+  mat_postmult_diag(&w->P, w->Dinv);
+  vec_mult_scalar(w->q, w->cinv, n);
+  vec_ew_prod(w->Dinv, w->q, w->q, n);
+  mat_premult_diag(&w->A, w->Einv);
+  mat_postmult_diag(&w->A, w->Dinv);
+  vec_ew_prod(w->Einv, w->l, w->l, m);
+  vec_ew_prod(w->Einv, w->u, w->u, m);
+}
+
+/* OSQP 0.6 update_rho_vec (auxil.c), called by osqp_update_{lower,upper}_bound: a constraint
+ * whose type changed gets the current settings rho, and the KKT matrix is refactored. */
+static int update_rho_vec(osqp_ws* w) {
+  int changed = 0;
+  for (int i = 0; i < w->m; ++i) {
+    int t;
+    if ((w->l[i] < -OSQP_INFTY * MIN_SCALING) && (w->u[i] > OSQP_INFTY * MIN_SCALING))
+      t = -1;
+    else if (w->u[i] - w->l[i] < RHO_TOL)
+      t = 1;
+    else
+      t = 0;
+    if (t == w->constr_type[i]) continue;
+    w->constr_type[i] = t;
+    w->rho_vec[i] = t == -1 ? RHO_MIN : t == 1 ? RHO_EQ_OVER_RHO_INEQ * w->rho : w->rho;
+    w->rho_inv_vec[i] = 1. / w->rho_vec[i];
+    changed = 1;
+  }
+  return changed ? factor_kkt(w) : 0;
+}
+
+/* OSQP 0.6 osqp_update_{lower,upper}_bound: replace, scale by E, check l <= u (a violation
+ * returns before update_rho_vec and is ignored by the reference), update_rho_vec. */
+static int update_bound(osqp_ws* w, double* dst, const double* src) {
+  const int m = w->m;
+  memcpy(dst, src, sizeof(double) * m);
+  if (w->st->scaling) vec_ew_prod(w->E, dst, dst, m);
+  for (int i = 0; i < m; ++i)
+    if (w->l[i] > w->u[i]) return 1;
+  return update_rho_vec(w);
+}
+
+/* OsqpEigen 0.6.3 Solver::updateHessianMatrix + updateGradient + updateLowerBound +
+ * updateUpperBound (A1RobotControl.cpp:532-535) on the QP of `rec`. */
+static int ws_update(osqp_ws* w, const double* rec) {
+  const int n = w->n, m = w->m;
+  double* Pd = (double*)malloc(sizeof(double) * (size_t)n * n);
+  double* qn = (double*)malloc(sizeof(double) * n);
+  double* ln = (double*)malloc(sizeof(double) * m);
+  double* un = (double*)malloc(sizeof(double) * m);
+  orc_build_qp(w->st, rec, Pd, qn, ln, un, NULL);
+  int fail = 0;
+  csc Pn = dense_to_csc_upper(Pd, n);
+  int same = Pn.p[n] == w->P.p[n];
+  for (int j = 0; same && j <= n; ++j) same = Pn.p[j] == w->P.p[j];
+  for (int k = 0; same && k < Pn.p[n]; ++k) same = Pn.i[k] == w->P.i[k];
+  if (same) {
+    /* osqp_update_P: unscale_data, new P values, scale_data (q, l, u and A are the old data,
+     * unscaled: the cost scaling c of this tick depends on the previous gradient), refactor */
+    if (w->st->scaling) unscale_data(w);
+    memcpy(w->P.x, Pn.x, sizeof(double) * Pn.p[n]);
+    if (w->st->scaling) scale_data(w);
+    fail |= factor_kkt(w);
+  } else {
+    /* sparsity changed: OsqpEigen re-initializes the solver and restores the unscaled primal
+     * and dual variables through osqp_warm_start_x / _y */
+    double* xu = (double*)malloc(sizeof(double) * n);
+    double* yu = (double*)malloc(sizeof(double) * m);
+    for (int i = 0; i < n; ++i) xu[i] = w->st->scaling ? w->D[i] * w->x[i] : w->x[i];
+    for (int i = 0; i < m; ++i) yu[i] = w->st->scaling ? (w->E[i] * w->y[i]) * w->cinv : w->y[i];
+    fail |= ws_setup(w, rec);
+    for (int i = 0; i < n; ++i) w->x[i] = w->st->scaling ? w->Dinv[i] * xu[i] : xu[i];
+    mat_vec(&w->A, w->x, w->z, 0);
+    for (int i = 0; i < m; ++i) w->y[i] = w->st->scaling ? w->c * (w->Einv[i] * yu[i]) : yu[i];
+    free(xu);
+    free(yu);
+  }
+  csc_free(&Pn);
+  /* osqp_update_lin_cost */
+  memcpy(w->q, qn, sizeof(double) * n);
+  if (w->st->scaling) {
+    vec_ew_prod(w->D, w->q, w->q, n);
+    vec_mult_scalar(w->q, w->c, n);
+  }
+  /* osqp_update_lower_bound, then osqp_update_upper_bound (no clipping on update) */
+  fail |= update_bound(w, w->l, ln);
+  fail |= update_bound(w, w->u, un);
+  free(Pd);
+  free(qn);
+  free(ln);
+  free(un);
+  return fail;
+}
+
+struct orc_solver {
+  osqp_ws w;
+  int initialized;
+  mpcqp_params prm;
+};
+
+orc_solver* orc_solver_new(const mpcqp_params* prm) {
+  orc_solver* s = (orc_solver*)calloc(1, sizeof(orc_solver));
+  s->prm = *prm;
+  return s;
+}
+void orc_solver_free(orc_solver* s) {
+  if (!s) return;
+  if (s->initialized) ws_free(&s->w);
+  free(s);
+}
+void orc_solver_reset(orc_solver* s) {
+  if (s->initialized) ws_free(&s->w);
+  s->initialized = 0;
+}
+
+int32_t orc_solver_step(orc_solver* s, const double* rec, mpcqp_result* res, double* sol,
+                        orc_trace_entry* trace, int32_t max_trace, int32_t* n_trace) {
+  const int N = s->prm.horizon;
+  memset(res, 0, sizeof(*res));
+  if (n_trace) *n_trace = 0;
+  if (record_has_nonfinite(rec, N)) { /* engine contract: state untouched, NaN result */
+    res->status = MPCQP_STATUS_NAN_INPUT;
+    res->nan_legs = 0xF;
+    if (sol)
+      for (int i = 0; i < ND * N; ++i) sol[i] = OSQP_NAN;
+    return MPCQP_OK;
+  }
+  int fail;
+  if (!s->initialized) {
+    ws_alloc(&s->w, &s->prm);
+    fail = ws_setup(&s->w, rec);
+    s->initialized = 1;
+  } else {
+    fail = ws_update(&s->w, rec);
+  }
+  ws_admm(&s->w, fail, trace, max_trace, n_trace);
+  ws_extract(&s->w, rec, res, sol);
+  return MPCQP_OK;
+}
+
+/* T ticks of `batch` independent robots: recs [T][batch][rec], res [T][batch]. */
+typedef struct {
+  const mpcqp_params* prm;
+  const double* recs;
+  mpcqp_result* res;
+  int T, batch, begin, end, rec_size;
+} seq_arg;
+static void* seq_worker(void* p) {
+  seq_arg* a = (seq_arg*)p;
+  for (int b = a->begin; b < a->end; ++b) {
+    orc_solver* s = orc_solver_new(a->prm);
+    for (int t = 0; t < a->T; ++t)
+      orc_solver_step(s, a->recs + ((size_t)t * a->batch + b) * a->rec_size, &a->res[(size_t)t * a->batch + b],
+                      NULL, NULL, 0, NULL);
+    orc_solver_free(s);
+  }
+  return NULL;
+}
+int32_t orc_solve_sequence(const mpcqp_params* prm, const double* recs, int32_t T, int32_t batch,
+                           mpcqp_result* res, int32_t nthreads) {
+  if (T < 0 || batch < 0 || nthreads < 1) return MPCQP_ERR_INVALID_ARG;
+  if (nthreads > batch) nthreads = batch > 0 ? batch : 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  seq_arg* args = (seq_arg*)malloc(sizeof(seq_arg) * nthreads);
+  for (int t = 0; t < nthreads; ++t) {
+    args[t].prm = prm;
+    args[t].recs = recs;
+    args[t].res = res;
+    args[t].T = T;
+    args[t].batch = batch;
+    args[t].begin = (int)((long long)batch * t / nthreads);
+    args[t].end = (int)((long long)batch * (t + 1) / nthreads);
+    args[t].rec_size = MPCQP_REC_SIZE(prm->horizon);
+    pthread_create(&th[t], NULL, seq_worker, &args[t]);
+  }
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  free(args);
   return MPCQP_OK;
 }
 

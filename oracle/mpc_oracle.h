@@ -55,6 +55,21 @@ int32_t orc_build_qp(const mpcqp_params* prm, const double* rec, double* P, doub
 int32_t orc_solve(const mpcqp_params* prm, const double* rec, mpcqp_result* res, double* sol,
                   orc_trace_entry* trace, int32_t max_trace, int32_t* n_trace);
 
+/* Warm start across control ticks: one persistent OSQP solver per robot, driven like the
+ * reference's member solver (A1RobotControl.h:67, A1RobotControl.cpp:520-540): the first step
+ * is initSolver + solve, later steps updateHessianMatrix / updateGradient / updateLowerBound /
+ * updateUpperBound + solve with warm_start (previous x, z, y and the adapted rho persist). */
+typedef struct orc_solver orc_solver;
+orc_solver* orc_solver_new(const mpcqp_params* prm);
+void orc_solver_free(orc_solver* s);
+void orc_solver_reset(orc_solver* s);
+int32_t orc_solver_step(orc_solver* s, const double* rec, mpcqp_result* res, double* sol,
+                        orc_trace_entry* trace, int32_t max_trace, int32_t* n_trace);
+/* T ticks x `batch` robots, each robot its own persistent solver: recs [T][batch][rec],
+ * res [T][batch]; robots partitioned over `nthreads` POSIX threads. */
+int32_t orc_solve_sequence(const mpcqp_params* prm, const double* recs, int32_t T, int32_t batch,
+                           mpcqp_result* res, int32_t nthreads);
+
 /* Batch over `nthreads` POSIX threads (static contiguous partition).  sols may be NULL. */
 int32_t orc_solve_batch(const mpcqp_params* prm, const double* recs, int32_t batch,
                         mpcqp_result* res, double* sols, int32_t nthreads);

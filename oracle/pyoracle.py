@@ -128,6 +128,19 @@ def lib():
         L.orc_solve_batch.argtypes = [ctypes.POINTER(Params), dp, ctypes.c_int32,
                                       ctypes.c_void_p, dp, ctypes.c_int32]
         L.orc_solve_batch.restype = ctypes.c_int32
+        L.orc_solver_new.argtypes = [ctypes.POINTER(Params)]
+        L.orc_solver_new.restype = ctypes.c_void_p
+        L.orc_solver_free.argtypes = [ctypes.c_void_p]
+        L.orc_solver_free.restype = None
+        L.orc_solver_reset.argtypes = [ctypes.c_void_p]
+        L.orc_solver_reset.restype = None
+        L.orc_solver_step.argtypes = [ctypes.c_void_p, dp, ctypes.POINTER(Result), dp,
+                                      ctypes.POINTER(TraceEntry), ctypes.c_int32,
+                                      ctypes.POINTER(ctypes.c_int32)]
+        L.orc_solver_step.restype = ctypes.c_int32
+        L.orc_solve_sequence.argtypes = [ctypes.POINTER(Params), dp, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_void_p, ctypes.c_int32]
+        L.orc_solve_sequence.restype = ctypes.c_int32
         _lib = L
     return _lib
 
@@ -186,3 +199,44 @@ def solve_batch(params, recs, nthreads=1, want_solution=False):
                                _dp(sols) if sols is not None else None, nthreads)
     assert rc == 0
     return (res, sols) if want_solution else res
+
+
+class WarmSolver:
+    """Persistent per-robot OSQP restatement (warm start across control ticks, orc_solver_*)."""
+
+    def __init__(self, params):
+        self.params = params
+        self._s = lib().orc_solver_new(ctypes.byref(params))
+
+    def step(self, rec):
+        N = self.params.horizon
+        res = Result()
+        sol = np.zeros(12 * N)
+        rec = np.ascontiguousarray(rec, dtype=np.float64)
+        rc = lib().orc_solver_step(self._s, _dp(rec), ctypes.byref(res), _dp(sol), None, 0, None)
+        assert rc == 0
+        return np.frombuffer(bytearray(res), dtype=RESULT_DTYPE)[0], sol
+
+    def reset(self):
+        lib().orc_solver_reset(self._s)
+
+    def close(self):
+        if self._s:
+            lib().orc_solver_free(self._s)
+            self._s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def solve_sequence(params, recs, nthreads=1):
+    """recs [T][B][rec]: each robot b solved over T ticks by its own warm-started solver."""
+    recs = np.ascontiguousarray(recs, dtype=np.float64)
+    T, B = recs.shape[0], recs.shape[1]
+    res = np.zeros((T, B), dtype=RESULT_DTYPE)
+    rc = lib().orc_solve_sequence(ctypes.byref(params), _dp(recs), T, B, res.ctypes.data, nthreads)
+    assert rc == 0
+    return res

@@ -36,14 +36,15 @@ def main():
             tr.fill_(float("nan"))
             s.solve_device_trace(d_rec.data_ptr(), a.batch, d_res.data_ptr(), 0, tr.data_ptr(), a.traced, stream)
         torch.cuda.synchronize()
-        marks = tr.cpu().numpy().reshape(a.traced, 128, 2)
+        marks = tr.cpu().numpy().reshape(a.traced, 64, 4)
         res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
-    phases = {"load": [], "condense": [], "ruiz": [], "tile_reload": [], "invert": [], "first_to_exit": [],
-              "total": [], "iter_cycles": []}
+    phases = {"load": [], "condense": [], "ruiz": [], "tile_reload": [], "invert": [],
+              "total": [], "iter_cycles": [], "shader_ghz": []}
     for b in range(a.traced):
         mk = marks[b]
         mk = mk[~np.isnan(mk[:, 0])]
         ids, cyc = mk[:, 0].astype(int), mk[:, 1]
+        phases["shader_ghz"].append((cyc[-1] - cyc[0]) / max(mk[-1, 2] - mk[0, 2], 1) * 0.1)
         at = {}
         for i, c in zip(ids, cyc):
             at.setdefault(i, []).append(c)

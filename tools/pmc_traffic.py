@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the solve kernel from a rocprofv3 counter pass.
+
+Collect in its own pass (no --sys-trace / --runtime-trace with --pmc):
+
+  rocprofv3 --pmc FETCH_SIZE WRITE_SIZE -d gpurun_out/pmc -o pmc -- \\
+      python3 bench.py --steps 3 --warmup 1 --no-cpu
+  python3 tools/pmc_traffic.py gpurun_out/pmc --key N10_B4096_trot
+
+Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
+doubled.  Access widths other than 16 B/lane are uncalibrated there: the result is an estimate
+(the JSON records both the raw and the corrected numbers).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse(d, kernel_substr):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection csv under {d}")
+    per = defaultdict(dict)  # dispatch id -> counter -> value
+    names = {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                kname = row.get("Kernel_Name", "")
+                if kernel_substr not in kname:
+                    continue
+                did = (fn, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+                per[did][row["Counter_Name"]] = float(row["Counter_Value"])
+                names[did] = kname
+    return per, names
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--key", default="N10_B4096_trot")
+    ap.add_argument("--kernel", default="solve_kernel")
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    a = ap.parse_args()
+    per, names = parse(a.dir, a.kernel)
+    rows = [v for v in per.values() if "FETCH_SIZE" in v and "WRITE_SIZE" in v]
+    if not rows:
+        print("no dispatch with both FETCH_SIZE and WRITE_SIZE", file=sys.stderr)
+        sys.exit(1)
+    rows = rows[1:] if len(rows) > 1 else rows  # drop the first (cold) dispatch
+    fetch_kib = sum(r["FETCH_SIZE"] for r in rows) / len(rows)
+    write_kib = sum(r["WRITE_SIZE"] for r in rows) / len(rows)
+    fetch_b = fetch_kib * 1024.0 * 2.0  # gfx950: FETCH_SIZE counts half of the bytes
+    write_b = write_kib * 1024.0
+    entry = {
+        "kernel": sorted(set(names.values()))[0],
+        "dispatches": len(rows),
+        "fetch_size_kib_raw": fetch_kib,
+        "write_size_kib_raw": write_kib,
+        "fetch_bytes_corrected": fetch_b,
+        "write_bytes": write_b,
+        "hbm_bytes_per_launch": fetch_b + write_b,
+        "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads), KiB -> B; other widths uncalibrated",
+    }
+    data = {}
+    if os.path.exists(a.out):
+        with open(a.out) as f:
+            data = json.load(f)
+    data[a.key] = entry
+    with open(a.out, "w") as f:
+        json.dump(data, f, indent=1)
+    print(json.dumps({a.key: entry}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
