@@ -3,8 +3,10 @@
 
 Collect in its own pass (no --sys-trace / --runtime-trace with --pmc):
 
-  rocprofv3 --pmc FETCH_SIZE WRITE_SIZE -d gpurun_out/pmc -o pmc -- \\
-      python3 bench.py --steps 3 --warmup 1 --no-cpu
+  rocprofv3 --pmc FETCH_SIZE --kernel-include-regex solve_kernel --output-format csv \\
+      -d gpurun_out/pmc/fetch -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu
+  rocprofv3 --pmc WRITE_SIZE ... -d gpurun_out/pmc/write ...   (FETCH_SIZE and WRITE_SIZE do not
+                                                               fit one pass on gfx950's TCC)
   python3 tools/pmc_traffic.py gpurun_out/pmc --key N10_B4096_trot
 
 Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE
@@ -49,13 +51,18 @@ def main():
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     per, names = parse(a.dir, a.kernel)
-    rows = [v for v in per.values() if "FETCH_SIZE" in v and "WRITE_SIZE" in v]
-    if not rows:
-        print("no dispatch with both FETCH_SIZE and WRITE_SIZE", file=sys.stderr)
-        sys.exit(1)
-    rows = rows[1:] if len(rows) > 1 else rows  # drop the first (cold) dispatch
-    fetch_kib = sum(r["FETCH_SIZE"] for r in rows) / len(rows)
-    write_kib = sum(r["WRITE_SIZE"] for r in rows) / len(rows)
+
+    def mean_of(counter):
+        vals = [v[counter] for v in per.values() if counter in v]
+        if not vals:
+            print(f"no dispatch with {counter}", file=sys.stderr)
+            sys.exit(1)
+        vals = vals[1:] if len(vals) > 1 else vals  # drop the first (cold) dispatch
+        return sum(vals) / len(vals), len(vals)
+
+    fetch_kib, nf = mean_of("FETCH_SIZE")
+    write_kib, nw = mean_of("WRITE_SIZE")
+    rows = [None] * min(nf, nw)
     fetch_b = fetch_kib * 1024.0 * 2.0  # gfx950: FETCH_SIZE counts half of the bytes
     write_b = write_kib * 1024.0
     entry = {
