@@ -18,8 +18,11 @@ struct mpcqp_handle {
   mpcqp_params p;
   int device = 0;
   int slots = 0;             // resident workgroups per device (occupancy x CUs), informational
+  int cus = 0;               // compute units of the device
   double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
+  size_t work_per = 0;       // doubles per instance the workspace was sized for
+  int path = 0;              // 0 auto, 1 dense K^-1 (horizon <= 10), 2 Riccati (mpcqp_debug_set_solver)
   // host wrapper staging
   double* d_recs = nullptr;
   mpcqp_result* d_res = nullptr;
@@ -48,6 +51,34 @@ bool params_valid(const mpcqp_params* p) {
   for (int i = 0; i < MPCQP_NUM_DOF; ++i)
     if (!isfinite(p->r_weights[i])) return false;
   return true;
+}
+
+bool use_riccati(const mpcqp_handle* h) {
+  return h->path == 2 || (h->path == 0 && h->p.horizon > mpcqp::DENSE_MAX_HORIZON);
+}
+size_t work_per_instance(const mpcqp_handle* h) {
+  return use_riccati(h) ? mpcqp::riccati_workspace_doubles(h->p.horizon) : mpcqp::workspace_doubles(h->p.horizon);
+}
+hipError_t occupancy_for(const mpcqp_handle* h, int* per_cu) {
+  return use_riccati(h) ? mpcqp::occupancy_riccati_any(h->p.horizon, per_cu)
+                        : mpcqp::occupancy_any(h->p.horizon, per_cu);
+}
+// (Re)size the per-instance workspace for `batch` instances of the current path.
+hipError_t ensure_workspace(mpcqp_handle* h, int32_t batch, void* stream) {
+  const size_t per = work_per_instance(h);
+  if ((size_t)batch <= h->work_cap && per <= h->work_per) return hipSuccess;
+  hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  if (e == hipSuccess) e = hipFree(h->work);
+  h->work = nullptr;
+  h->work_cap = 0;
+  h->work_per = 0;
+  const size_t cap = (size_t)batch > h->work_cap ? (size_t)batch : h->work_cap;
+  if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * per * cap);
+  if (e == hipSuccess) {
+    h->work_cap = cap;
+    h->work_per = per;
+  }
+  return e;
 }
 
 }  // namespace
@@ -100,10 +131,11 @@ int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** 
   if (e != hipSuccess) { delete h; return MPCQP_ERR_HIP; }
   int cus = 0, per_cu = 0;
   e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-  if (e == hipSuccess) e = mpcqp::occupancy_any(params->horizon, &per_cu);
+  if (e == hipSuccess) e = occupancy_for(h, &per_cu);
   if (e != hipSuccess || cus <= 0) { delete h; return MPCQP_ERR_HIP; }
   if (per_cu < 1) per_cu = 1;
   h->slots = cus * per_cu;
+  h->cus = cus;
   *out = h;
   return MPCQP_OK;
 }
@@ -126,16 +158,9 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   if (batch == 0) return MPCQP_OK;
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
-  if ((size_t)batch > h->work_cap) {
-    // grow-only; a capture-safe caller pre-sizes with mpcqp_reserve()
-    e = hipStreamSynchronize((hipStream_t)stream);
-    if (e == hipSuccess) e = hipFree(h->work);
-    h->work = nullptr;
-    h->work_cap = 0;
-    if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * mpcqp::workspace_doubles(h->p.horizon) * batch);
-    if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
-    h->work_cap = batch;
-  }
+  // grow-only; a capture-safe caller pre-sizes with mpcqp_reserve()
+  e = ensure_workspace(h, batch, stream);
+  if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
   mpcqp::LaunchArgs a;
   a.recs = d_records;
   a.batch = batch;
@@ -147,7 +172,7 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   a.grid = batch;
   a.stream = stream;
   a.p = h->p;
-  e = mpcqp::launch_solve_any(a);
+  e = use_riccati(h) ? mpcqp::launch_riccati_any(a) : mpcqp::launch_solve_any(a);
   if (e != hipSuccess) return set_hip_error(h, e, "solve_kernel launch");
   return MPCQP_OK;
 }
@@ -251,17 +276,33 @@ int32_t mpcqp_handle_slots(mpcqp_handle* h) { return h ? h->slots : 0; }
 
 int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {
   if (!h || batch < 0) return MPCQP_ERR_INVALID_ARG;
-  if ((size_t)batch <= h->work_cap) return MPCQP_OK;
   hipError_t e = hipSetDevice(h->device);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipFree(h->work);
-  h->work = nullptr;
-  h->work_cap = 0;
-  if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * mpcqp::workspace_doubles(h->p.horizon) * batch);
+  if (e == hipSuccess && ((size_t)batch > h->work_cap || work_per_instance(h) > h->work_per))
+    e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = ensure_workspace(h, batch, nullptr);
   if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
-  h->work_cap = batch;
   return MPCQP_OK;
 }
-int32_t mpcqp_solve_threads(int32_t horizon) { return mpcqp::solve_threads(horizon); }
+int32_t mpcqp_solve_threads(int32_t horizon) {
+  if (horizon < 1 || horizon > MPCQP_MAX_HORIZON) return 0;
+  return horizon > mpcqp::DENSE_MAX_HORIZON ? mpcqp::riccati_threads(horizon) : mpcqp::solve_threads(horizon);
+}
+
+int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
+  if (!h || path < 0 || path > 2) return MPCQP_ERR_INVALID_ARG;
+  if (path == 1 && h->p.horizon > mpcqp::DENSE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
+  const int old = h->path;
+  h->path = path;
+  int per_cu = 0;
+  e = occupancy_for(h, &per_cu);
+  if (e != hipSuccess) {
+    h->path = old;
+    return set_hip_error(h, e, "occupancy query");
+  }
+  h->slots = per_cu * h->cus;
+  return MPCQP_OK;
+}
 
 }  // extern "C"

@@ -28,4 +28,11 @@ hipError_t occupancy_any(int horizon, int* blocks);
 int solve_threads(int horizon);
 size_t workspace_doubles(int horizon);  // per robot
 
+// Riccati-factored path (mpcqp_riccati.hip): horizons 11..20, and any horizon on request
+hipError_t launch_riccati_any(const LaunchArgs& a);
+hipError_t occupancy_riccati_any(int horizon, int* blocks);
+int riccati_threads(int horizon);
+size_t riccati_workspace_doubles(int horizon);  // per robot
+constexpr int DENSE_MAX_HORIZON = 10;
+
 }  // namespace mpcqp

@@ -14,7 +14,9 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(PKG_ROOT, "lib", "libmpcqp.so")
 
 STATE_DIM, NUM_LEG, NUM_DOF, CONSTRAINT_DIM = 13, 4, 12, 20
-MAX_HORIZON = 10
+MAX_HORIZON = 20
+DENSE_MAX_HORIZON = 10  # horizons above run the Riccati path
+SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI = 0, 1, 2
 OSQP_INFTY = 1e30
 
 # record layout (include/mpcqp.h MPCQP_REC_*)
@@ -83,6 +85,7 @@ EXPORTED = [
     "mpcqp_solve_batch_device", "mpcqp_solve_batch_host", "mpcqp_build_qp_device",
     "mpcqp_status_str", "mpcqp_error_str", "mpcqp_last_error",
     "mpcqp_debug_solve_trace_device", "mpcqp_abi_sizes", "mpcqp_handle_slots", "mpcqp_solve_threads",
+    "mpcqp_debug_set_solver",
 ]
 
 _lib = None
@@ -131,6 +134,8 @@ def load():
     L.mpcqp_handle_slots.restype = i32
     L.mpcqp_solve_threads.argtypes = [i32]
     L.mpcqp_solve_threads.restype = i32
+    L.mpcqp_debug_set_solver.argtypes = [vp, i32]
+    L.mpcqp_debug_set_solver.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):

@@ -48,6 +48,10 @@ class MpcQpSolver:
     def slots(self):
         return self._L.mpcqp_handle_slots(self._h)
 
+    def set_solver(self, path):
+        """mpcqp_debug_set_solver: 0 auto, 1 dense K^-1 (N <= 10), 2 Riccati."""
+        check(self._L.mpcqp_debug_set_solver(self._h, int(path)), self._h, "mpcqp_debug_set_solver")
+
     def reserve(self, batch):
         check(self._L.mpcqp_reserve(self._h, int(batch)), self._h, "mpcqp_reserve")
 

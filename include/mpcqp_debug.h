@@ -25,8 +25,13 @@ int32_t mpcqp_abi_sizes(int32_t* params_size, int32_t* result_size);
 /* Persistent-grid size (resident workgroups) chosen for the handle's device. */
 int32_t mpcqp_handle_slots(mpcqp_handle* h);
 
-/* Threads per robot workgroup of the solve kernel for horizon N (one 16-lane group per foot). */
+/* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */
 int32_t mpcqp_solve_threads(int32_t horizon);
+
+/* Select the linear-system path of a handle: 0 auto (dense K^-1 for N <= 10, Riccati above),
+ * 1 dense (N <= 10 only), 2 Riccati (any N).  Both paths run the same OSQP iteration; the
+ * selection exists to cross-check them on the same inputs. */
+int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path);
 
 #ifdef __cplusplus
 }

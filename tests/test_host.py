@@ -50,9 +50,10 @@ def test_test_mpc_assembly_matches_oracle(oracle):
 
 def test_record_layout():
     L = _lib.load()
-    for N in range(1, 11):
+    for N in range(1, 21):
         assert L.mpcqp_record_size(N) == _lib.rec_size(N) == 44 + 25 * N + (N & 1)
     assert L.mpcqp_record_size(0) == 0
+    assert L.mpcqp_solve_threads(21) == 0 and L.mpcqp_solve_threads(20) > 0
 
 
 def test_default_params_are_reference_settings():
@@ -101,7 +102,7 @@ def test_abi_struct_sizes():
 def test_invalid_params_rejected_before_device():
     L = _lib.load()
     h = ctypes.c_void_p()
-    for bad in (dict(horizon=0), dict(horizon=11), dict(adaptive_rho_interval=0), dict(alpha=2.5),
+    for bad in (dict(horizon=0), dict(horizon=21), dict(adaptive_rho_interval=0), dict(alpha=2.5),
                 dict(rho=-1.0), dict(scaled_termination=1)):
         p = mpcqp.default_params(10)
         for k, v in bad.items():
