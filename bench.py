@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=2048, help="instances timed on the CPU oracle")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--solver", default="auto", choices=["auto", "dense", "riccati", "wave"],
+                    help="linear-system path (mpcqp_debug_set_solver); auto = the library default")
     args = ap.parse_args()
 
     import torch
@@ -85,6 +87,9 @@ def main():
     config_id = 1 if (args.gait == "trot" and not args.mixed_mu) else 4
     params = mpcqp.default_params(N)
     solver = mpcqp.MpcQpSolver(params, device=local_rank)
+    path = {"auto": 0, "dense": 1, "riccati": 2, "wave": 3}[args.solver]
+    if path:
+        solver.set_solver(path)
     solver.reserve(B)
 
     # synthetic Go1 states, seed = config*1000 + rank; records resident in HBM

@@ -22,7 +22,7 @@ struct mpcqp_handle {
   double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
   size_t work_per = 0;       // doubles per instance the workspace was sized for
-  int path = 0;              // 0 auto, 1 dense K^-1 (horizon <= 10), 2 Riccati (mpcqp_debug_set_solver)
+  int path = 0;              // 0 auto, 1 dense K^-1, 2 Riccati workgroup, 3 Riccati wave (mpcqp_debug_set_solver)
   // host wrapper staging
   double* d_recs = nullptr;
   mpcqp_result* d_res = nullptr;
@@ -53,19 +53,29 @@ bool params_valid(const mpcqp_params* p) {
   return true;
 }
 
-bool use_riccati(const mpcqp_handle* h) {
-  return h->path == 2 || (h->path == 0 && h->p.horizon > mpcqp::DENSE_MAX_HORIZON);
+// 1 dense K^-1, 2 Riccati (one workgroup per robot), 3 Riccati (one wave per robot)
+int effective_path(const mpcqp_handle* h) {
+  if (h->path != 0) return h->path;
+  return h->p.horizon > mpcqp::DENSE_MAX_HORIZON ? 2 : 1;
 }
 size_t work_per_instance(const mpcqp_handle* h) {
-  return use_riccati(h) ? mpcqp::riccati_workspace_doubles(h->p.horizon) : mpcqp::workspace_doubles(h->p.horizon);
+  switch (effective_path(h)) {
+    case 1: return mpcqp::workspace_doubles(h->p.horizon);
+    case 2: return mpcqp::riccati_workspace_doubles(h->p.horizon);
+    default: return 0;  // the wave kernel keeps everything on chip
+  }
 }
 hipError_t occupancy_for(const mpcqp_handle* h, int* per_cu) {
-  return use_riccati(h) ? mpcqp::occupancy_riccati_any(h->p.horizon, per_cu)
-                        : mpcqp::occupancy_any(h->p.horizon, per_cu);
+  switch (effective_path(h)) {
+    case 1: return mpcqp::occupancy_any(h->p.horizon, per_cu);
+    case 2: return mpcqp::occupancy_riccati_any(h->p.horizon, per_cu);
+    default: return mpcqp::occupancy_wave_any(h->p.horizon, per_cu);
+  }
 }
 // (Re)size the per-instance workspace for `batch` instances of the current path.
 hipError_t ensure_workspace(mpcqp_handle* h, int32_t batch, void* stream) {
   const size_t per = work_per_instance(h);
+  if (per == 0) return hipSuccess;
   if ((size_t)batch <= h->work_cap && per <= h->work_per) return hipSuccess;
   hipError_t e = hipStreamSynchronize((hipStream_t)stream);
   if (e == hipSuccess) e = hipFree(h->work);
@@ -172,7 +182,11 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   a.grid = batch;
   a.stream = stream;
   a.p = h->p;
-  e = use_riccati(h) ? mpcqp::launch_riccati_any(a) : mpcqp::launch_solve_any(a);
+  switch (effective_path(h)) {
+    case 1: e = mpcqp::launch_solve_any(a); break;
+    case 2: e = mpcqp::launch_riccati_any(a); break;
+    default: e = mpcqp::launch_wave_any(a); break;
+  }
   if (e != hipSuccess) return set_hip_error(h, e, "solve_kernel launch");
   return MPCQP_OK;
 }
@@ -289,8 +303,9 @@ int32_t mpcqp_solve_threads(int32_t horizon) {
 }
 
 int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
-  if (!h || path < 0 || path > 2) return MPCQP_ERR_INVALID_ARG;
+  if (!h || path < 0 || path > 3) return MPCQP_ERR_INVALID_ARG;
   if (path == 1 && h->p.horizon > mpcqp::DENSE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
+  if (path == 3 && h->p.horizon > mpcqp::WAVE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
   const int old = h->path;
@@ -303,6 +318,11 @@ int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
   }
   h->slots = per_cu * h->cus;
   return MPCQP_OK;
+}
+
+int32_t mpcqp_debug_wave_selftest(double* d_out, void* stream) {
+  if (!d_out) return MPCQP_ERR_INVALID_ARG;
+  return mpcqp::wave_selftest(d_out, stream) == hipSuccess ? MPCQP_OK : MPCQP_ERR_HIP;
 }
 
 }  // extern "C"

@@ -35,4 +35,10 @@ int riccati_threads(int horizon);
 size_t riccati_workspace_doubles(int horizon);  // per robot
 constexpr int DENSE_MAX_HORIZON = 10;
 
+// One-wave-per-robot Riccati path (mpcqp_wave.hip): horizons 1..WAVE_MAX_HORIZON
+hipError_t launch_wave_any(const LaunchArgs& a);
+hipError_t occupancy_wave_any(int horizon, int* blocks);
+hipError_t wave_selftest(double* d_out, void* stream);
+constexpr int WAVE_MAX_HORIZON = 10;
+
 }  // namespace mpcqp

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(PKG_ROOT, "lib", "libmpcq
 STATE_DIM, NUM_LEG, NUM_DOF, CONSTRAINT_DIM = 13, 4, 12, 20
 MAX_HORIZON = 20
 DENSE_MAX_HORIZON = 10  # horizons above run the Riccati path
-SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI = 0, 1, 2
+SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI, SOLVER_WAVE = 0, 1, 2, 3
 OSQP_INFTY = 1e30
 
 # record layout (include/mpcqp.h MPCQP_REC_*)
@@ -85,7 +85,7 @@ EXPORTED = [
     "mpcqp_solve_batch_device", "mpcqp_solve_batch_host", "mpcqp_build_qp_device",
     "mpcqp_status_str", "mpcqp_error_str", "mpcqp_last_error",
     "mpcqp_debug_solve_trace_device", "mpcqp_abi_sizes", "mpcqp_handle_slots", "mpcqp_solve_threads",
-    "mpcqp_debug_set_solver",
+    "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest",
 ]
 
 _lib = None
@@ -136,6 +136,8 @@ def load():
     L.mpcqp_solve_threads.restype = i32
     L.mpcqp_debug_set_solver.argtypes = [vp, i32]
     L.mpcqp_debug_set_solver.restype = i32
+    L.mpcqp_debug_wave_selftest.argtypes = [vp, vp]
+    L.mpcqp_debug_wave_selftest.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):

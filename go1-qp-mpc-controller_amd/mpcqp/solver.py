@@ -49,7 +49,7 @@ class MpcQpSolver:
         return self._L.mpcqp_handle_slots(self._h)
 
     def set_solver(self, path):
-        """mpcqp_debug_set_solver: 0 auto, 1 dense K^-1 (N <= 10), 2 Riccati."""
+        """mpcqp_debug_set_solver: 0 auto, 1 dense K^-1 (N <= 10), 2 Riccati workgroup, 3 Riccati wave."""
         check(self._L.mpcqp_debug_set_solver(self._h, int(path)), self._h, "mpcqp_debug_set_solver")
 
     def reserve(self, batch):

@@ -28,10 +28,13 @@ int32_t mpcqp_handle_slots(mpcqp_handle* h);
 /* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */
 int32_t mpcqp_solve_threads(int32_t horizon);
 
-/* Select the linear-system path of a handle: 0 auto (dense K^-1 for N <= 10, Riccati above),
- * 1 dense (N <= 10 only), 2 Riccati (any N).  Both paths run the same OSQP iteration; the
- * selection exists to cross-check them on the same inputs. */
+/* Select the linear-system path of a handle: 0 auto, 1 dense K^-1 (N <= 10), 2 Riccati with
+ * one workgroup per robot (any N), 3 Riccati with one wavefront per robot (N <= 10).  All paths
+ * run the same OSQP iteration; the selection exists to cross-check them on the same inputs. */
 int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path);
+
+/* Cross-lane primitive self-test of the wave path: writes 6 x 64 doubles to d_out (device). */
+int32_t mpcqp_debug_wave_selftest(double* d_out, void* stream);
 
 #ifdef __cplusplus
 }
