@@ -31,8 +31,7 @@
 // The four lanes of a leg hold the foot's constraint rows: friction-pyramid rows 0-3 (one per
 // lane) and row 4 (fz bounds, replicated), so every per-foot ADMM operation (A~x, A~'y, the
 // projection) is a quad-perm DPP.  No barrier exists anywhere: the workgroup is the wave.
-// Setup (condensation, Ruiz) keeps |H| as fp32 in LDS for the column norms only;
-// everything else is binary64.
+// Arithmetic is binary64 throughout.
 #include "mpcqp_device.h"
 
 namespace mpcqp {
@@ -51,26 +50,23 @@ struct Cfg {
 template <int N>
 struct WSmem {
   using C = Cfg<N>;
-  double rec[C::REC];
+  static constexpr int NK = N > 1 ? N - 1 : 1;  // K_k stored for k = 1..N-1
+  static constexpr int NA = N > 2 ? N - 2 : 1;  // Acl_k stored for k = 1..N-2
   alignas(16) double Bw[N][3][ND];  // rows 6-8 of B_d(k) = I_w^-1 skew(foot) dt (rows 9-11: dt/m I)
-  double lam[N][ND];                // gradient adjoint lambda_k (states 0..11)
-  double vec[2][16];                // sequential 13-vectors (gradient forward sweep)
   union U {
-    struct Hs {  // setup: |H| (fp32, packed upper triangle, column-major), S_k B_k, Ruiz vectors
-      float H32[C::NH];
-      float D32[C::n];
-      alignas(16) double G[N][144];
-      alignas(16) double V[2][144];
-      double S[144], T[144];
-      double D[C::n], Dt[C::n], q[C::n], cm[C::n], E[C::m];
-      double ak[C::m][3];
+    struct Hs {  // setup: record, Ruiz vectors
+      double rec[C::REC];
+      double D[C::n], Dt[C::n], q[C::n], E[C::m];
+      double lam[N][ND];  // gradient adjoint lambda_k (states 0..11)
+      double vec[2][16];  // sequential 13-vectors (gradient forward sweep)
     } h;
     struct Fs {  // solve: per-step factors + factorization scratch
       alignas(16) double Gi[N][144];
-      alignas(16) double K[N][144];
-      alignas(16) double Acl[N][144];
-      alignas(16) double P[144], PB[144], PA[144], F[144], Gm[144];
-      double Rt[N][ND][3];  // R'_k: row i, the three columns of its foot block
+      alignas(16) double K[NK][144];
+      alignas(16) double Acl[NA][144];
+      alignas(16) double P[144], PA[144], F[144];
+      alignas(16) double xch[2][36];  // block Gauss-Jordan pivot block rows (double-buffered)
+      double Rt[N][4][6];             // R'_k foot blocks, upper triangle (00 01 02 11 12 22)
     } f;
   } u;
 };
@@ -78,31 +74,82 @@ struct WSmem {
 // ---- cross-lane primitives ---------------------------------------------------------------------
 #define WV_FM(A, M, L) "v_fmac_f64_dpp " A ", %[x], " M " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
 // y_i = sum_c M[i][c] x_c, x_c broadcast from lane 4(c/3)+c%3 of each DPP row, M row i in `c`.
-// Two accumulators (even / odd c).  s_nop 1: a VALU write of x just before needs 2 wait states
-// before a DPP read of it.
+// Hazards (the compiler cannot see into the asm): a DPP instruction needs 2 wait states after a
+// VALU write of ANY of its VGPR operands and 5 after an EXEC write.  Hence the leading s_nop 4 and
+// three accumulators in rotation (each is re-read 3 instructions after it was written).
 __device__ __forceinline__ double mv12(double x, const double (&c)[12]) {
-  double a0 = 0.0, a1 = 0.0;
-  asm("s_nop 1\n\t"
-      WV_FM("%[a0]", "%[c0]", 0) WV_FM("%[a1]", "%[c1]", 1) WV_FM("%[a0]", "%[c2]", 2)
-      WV_FM("%[a1]", "%[c3]", 4) WV_FM("%[a0]", "%[c4]", 5) WV_FM("%[a1]", "%[c5]", 6)
-      WV_FM("%[a0]", "%[c6]", 8) WV_FM("%[a1]", "%[c7]", 9) WV_FM("%[a0]", "%[c8]", 10)
-      WV_FM("%[a1]", "%[c9]", 12) WV_FM("%[a0]", "%[c10]", 13) WV_FM("%[a1]", "%[c11]", 14)
-      : [a0] "+v"(a0), [a1] "+v"(a1)
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  asm("s_nop 4\n\t"
+      WV_FM("%[a0]", "%[c0]", 0) WV_FM("%[a1]", "%[c1]", 1) WV_FM("%[a2]", "%[c2]", 2)
+      WV_FM("%[a0]", "%[c3]", 4) WV_FM("%[a1]", "%[c4]", 5) WV_FM("%[a2]", "%[c5]", 6)
+      WV_FM("%[a0]", "%[c6]", 8) WV_FM("%[a1]", "%[c7]", 9) WV_FM("%[a2]", "%[c8]", 10)
+      WV_FM("%[a0]", "%[c9]", 12) WV_FM("%[a1]", "%[c10]", 13) WV_FM("%[a2]", "%[c11]", 14)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
       : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
         [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]),
         [c11] "v"(c[11]));
-  return a0 + a1;
+  return (a0 + a1) + a2;
 }
 // sum over states 6..11 (lanes 8, 9, 10, 12, 13, 14) of c[s-6] x_s
 __device__ __forceinline__ double mv6(double x, const double (&c)[6]) {
-  double a0 = 0.0, a1 = 0.0;
-  asm("s_nop 1\n\t"
-      WV_FM("%[a0]", "%[c0]", 8) WV_FM("%[a1]", "%[c1]", 9) WV_FM("%[a0]", "%[c2]", 10)
-      WV_FM("%[a1]", "%[c3]", 12) WV_FM("%[a0]", "%[c4]", 13) WV_FM("%[a1]", "%[c5]", 14)
-      : [a0] "+v"(a0), [a1] "+v"(a1)
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  asm("s_nop 4\n\t"
+      WV_FM("%[a0]", "%[c0]", 8) WV_FM("%[a1]", "%[c1]", 9) WV_FM("%[a2]", "%[c2]", 10)
+      WV_FM("%[a0]", "%[c3]", 12) WV_FM("%[a1]", "%[c4]", 13) WV_FM("%[a2]", "%[c5]", 14)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
       : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
         [c5] "v"(c[5]));
-  return a0 + a1;
+  return (a0 + a1) + a2;
+}
+// Two / three independent mat-vecs interleaved in one block (each has its own x and rows); every
+// accumulator is re-read 4 (x2) or 6 (x3) instructions after its last write.
+#define WV_T2(L, I, J) WV_FX("%[a" #J "]", "%[x0]", "%[p" #I "]", L) WV_FX("%[b" #J "]", "%[x1]", "%[q" #I "]", L)
+#define WV_T3(L, I, J) WV_T2(L, I, J) WV_FX("%[d" #J "]", "%[x2]", "%[r" #I "]", L)
+#define WV_FX(A, X, M, L) "v_fmac_f64_dpp " A ", " X ", " M " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#define WV_OPS12(P, C) [P##0] "v"(C[0]), [P##1] "v"(C[1]), [P##2] "v"(C[2]), [P##3] "v"(C[3]), [P##4] "v"(C[4]), \
+    [P##5] "v"(C[5]), [P##6] "v"(C[6]), [P##7] "v"(C[7]), [P##8] "v"(C[8]), [P##9] "v"(C[9]),                \
+    [P##10] "v"(C[10]), [P##11] "v"(C[11])
+__device__ __forceinline__ void mv12x2(double x0, double x1, const double (&c0)[12], const double (&c1)[12],
+                                       double& y0, double& y1) {
+  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+  asm("s_nop 4\n\t"
+      WV_T2(0, 0, 0) WV_T2(1, 1, 1) WV_T2(2, 2, 0) WV_T2(4, 3, 1) WV_T2(5, 4, 0) WV_T2(6, 5, 1)
+      WV_T2(8, 6, 0) WV_T2(9, 7, 1) WV_T2(10, 8, 0) WV_T2(12, 9, 1) WV_T2(13, 10, 0) WV_T2(14, 11, 1)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [b0] "+v"(b0), [b1] "+v"(b1)
+      : [x0] "v"(x0), [x1] "v"(x1), WV_OPS12(p, c0), WV_OPS12(q, c1));
+  y0 = a0 + a1;
+  y1 = b0 + b1;
+}
+__device__ __forceinline__ void mv12x3(double x0, double x1, double x2, const double (&c0)[12],
+                                       const double (&c1)[12], const double (&c2)[12], double& y0, double& y1,
+                                       double& y2) {
+  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0, d0 = 0.0, d1 = 0.0;
+  asm("s_nop 4\n\t"
+      WV_T3(0, 0, 0) WV_T3(1, 1, 1) WV_T3(2, 2, 0) WV_T3(4, 3, 1) WV_T3(5, 4, 0) WV_T3(6, 5, 1)
+      WV_T3(8, 6, 0) WV_T3(9, 7, 1) WV_T3(10, 8, 0) WV_T3(12, 9, 1) WV_T3(13, 10, 0) WV_T3(14, 11, 1)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [b0] "+v"(b0), [b1] "+v"(b1), [d0] "+v"(d0), [d1] "+v"(d1)
+      : [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), WV_OPS12(p, c0), WV_OPS12(q, c1), WV_OPS12(r, c2));
+  y0 = a0 + a1;
+  y1 = b0 + b1;
+  y2 = d0 + d1;
+}
+#undef WV_T2
+#undef WV_T3
+#undef WV_FX
+#undef WV_OPS12
+// y[r] = M_r x[r] for the R register rounds of a parallel phase, interleaved.
+template <int R>
+__device__ __forceinline__ void mv_rounds(const double (&x)[R], const double (&c)[R][12], double (&y)[R]) {
+  if constexpr (R == 1) {
+    y[0] = mv12(x[0], c[0]);
+  } else if constexpr (R == 2) {
+    mv12x2(x[0], x[1], c[0], c[1], y[0], y[1]);
+  } else if constexpr (R == 3) {
+    mv12x3(x[0], x[1], x[2], c[0], c[1], c[2], y[0], y[1], y[2]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) y[r] = mv12(x[r], c[r]);
+  }
 }
 #undef WV_FM
 
@@ -258,77 +305,162 @@ __device__ __forceinline__ double quad_at(double v, double v4, double AK0, doubl
   return a < 2 ? s01 : s2;
 }
 
-// ---- factorization of c B'Q̄B + R' (LDS, one wave; R' in F.Rt) ------------------------------------
+// ---- factorization of c B'Q̄B + R' (one wave; R' in F.Rt) ------------------------------------------
+// Lanes 0..47 own (row i = t / 4, foot-column block g = t % 4): entries [i][3g..3g+2] of every 12x12
+// product, so the four lanes of row i form a quad and the 3x3 block (i / 3, g) is a foot block.
+// G^-1 is a block Gauss-Jordan with the 3x3 foot blocks as pivots: the pivot block row goes
+// through LDS (one wave-sync per pivot), the pivot column is a quad broadcast.
+__device__ __forceinline__ void inv3(const double (&M)[9], double (&I)[9]) {  // Eigen-style cofactor inverse
+  auto cof = [&](int i, int j) __attribute__((always_inline)) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return M[i1 * 3 + j1] * M[i2 * 3 + j2] - M[i1 * 3 + j2] * M[i2 * 3 + j1];
+  };
+  const double det = (cof(0, 0) * M[0] + cof(1, 0) * M[3]) + cof(2, 0) * M[6];
+  const double id = 1.0 / det;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) I[j * 3 + i] = cof(i, j) * id;
+}
+
+// index of (r, c) in a symmetric 3x3 stored as its upper triangle 00 01 02 11 12 22
+__device__ __forceinline__ int sym6(int r, int c) {
+  const int lo = r < c ? r : c, hi = r < c ? c : r;
+  return lo == 0 ? hi : (lo == 1 ? 2 + hi : 5);
+}
+// quad broadcast of lane j (j a constant after unrolling)
+__device__ __forceinline__ double qbcast(double v, int j) {
+  switch (j) {
+    case 0: return dpp<0x00>(v);
+    case 1: return dpp<0x55>(v);
+    case 2: return dpp<0xAA>(v);
+    default: return dpp<0xFF>(v);
+  }
+}
+
 template <int N>
 __device__ void factorize(WSmem<N>& sm, const mpcqp_params& p, const Adisc& A, double c, double dtm) {
   auto& F = sm.u.f;
   const int t = threadIdx.x;
+  const bool act = t < 48;
+  const int i = act ? t >> 2 : 11, g = t & 3, ib = i / 3;
   for (int e = t; e < 144; e += NT) {
-    const int i = e / 12, j = e % 12;
-    F.P[e] = (i == j) ? c * (2.0 * p.q_weights[i]) : 0.0;
-    F.K[0][e] = 0.0;
-    F.Acl[0][e] = 0.0;
-    F.Acl[N - 1][e] = 0.0;
+    const int r = e / 12, j = e % 12;
+    F.P[e] = (r == j) ? c * (2.0 * p.q_weights[r]) : 0.0;
   }
   wave_sync();
   for (int k = N - 1; k >= 0; --k) {
-    for (int e = t; e < 144; e += NT) {  // PB = P B_k, PA = P A
-      const int r = e / 12, j = e % 12;
-      F.PB[e] = mb(sm, F.P, k, r, j, dtm);
-      if (k >= 1) F.PA[e] = A.ma(F.P, r, j);
+    // B_k column i (rows 6, 7, 8 and 9 + i%3) and, per owned column cc, B_k column cc
+    const double bi0 = sm.Bw[k][0][i], bi1 = sm.Bw[k][1][i], bi2 = sm.Bw[k][2][i];
+    const int si = 9 + i % 3;
+    double Gv[3], PAv[3];
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      const int cc = 3 * g + jj;
+      const double bc0 = sm.Bw[k][0][cc], bc1 = sm.Bw[k][1][cc], bc2 = sm.Bw[k][2][cc];
+      auto pb = [&](int s) __attribute__((always_inline)) {  // (P B_k)[s][cc]
+        const double* pr = F.P + 12 * s;
+        return ((pr[6] * bc0 + pr[7] * bc1) + pr[8] * bc2) + pr[9 + jj] * dtm;
+      };
+      const double gs = ((bi0 * pb(6) + bi1 * pb(7)) + bi2 * pb(8)) + dtm * pb(si);
+      Gv[jj] = ((ib == g) ? F.Rt[k][ib][sym6(i % 3, jj)] : 0.0) + gs;  // G = R'_k + B_k' P B_k
+      PAv[jj] = A.ma(F.P, i, cc);                         // P A
     }
-    wave_sync();
-    for (int e = t; e < 144; e += NT) {  // G = R'_k + B_k' PB, F = B_k' PA
-      const int i = e / 12, j = e % 12;
-      const double rt = (i / 3 == j / 3) ? F.Rt[k][i][j % 3] : 0.0;
-      F.Gm[e] = rt + btm(sm, F.PB, k, i, j, dtm);
-      if (k >= 1) F.F[e] = btm(sm, F.PA, k, i, j, dtm);
-    }
-    wave_sync();
-    {  // G^-1 by Gauss-Jordan (SPD, no pivoting); entries t, t+64, t+128 (< 144)
-      double* G = F.Gm;
-      for (int piv = 0; piv < 12; ++piv) {
-        const double dinv = 1.0 / G[piv * 12 + piv];
-        auto gj = [&](int e) __attribute__((always_inline)) {
-          const int i = e / 12, j = e % 12;
-          if (i == piv && j == piv) return dinv;
-          if (i == piv) return G[piv * 12 + j] * dinv;
-          if (j == piv) return -G[i * 12 + piv] * dinv;
-          return G[i * 12 + j] - G[i * 12 + piv] * (G[piv * 12 + j] * dinv);
-        };
-        const double u0 = gj(t), u1 = gj(t + 64);
-        const double u2 = t + 128 < 144 ? gj(t + 128) : 0.0;
-        wave_sync();
-        G[t] = u0;
-        G[t + 64] = u1;
-        if (t + 128 < 144) G[t + 128] = u2;
-        wave_sync();
+    if (k >= 1 && act)
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) F.PA[12 * i + 3 * g + jj] = PAv[jj];
+    // block Gauss-Jordan: G <- G^-1
+#pragma unroll
+    for (int pv = 0; pv < 4; ++pv) {
+      double* xb = F.xch[pv & 1];
+      if (act && ib == pv)
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) xb[12 * (i % 3) + 3 * g + jj] = Gv[jj];
+      wave_sync();
+      double Mpp[9], Pinv[9], Mpg[9];
+#pragma unroll
+      for (int e = 0; e < 9; ++e) {
+        Mpp[e] = xb[12 * (e / 3) + 3 * pv + e % 3];
+        Mpg[e] = xb[12 * (e / 3) + 3 * g + e % 3];
       }
-      for (int e = t; e < 144; e += NT) F.Gi[k][e] = G[e];
+      inv3(Mpp, Pinv);
+      // my row of block (ib, pv): quad broadcast of lane pv
+      double gi[3];
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) gi[jj] = qbcast(Gv[jj], pv);
+      const int rr = i % 3;
+      if (ib == pv) {
+        const double pi0 = sel3(rr, Pinv[0], Pinv[3], Pinv[6]), pi1 = sel3(rr, Pinv[1], Pinv[4], Pinv[7]),
+                     pi2 = sel3(rr, Pinv[2], Pinv[5], Pinv[8]);
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+          const double pr = (pi0 * Mpg[jj] + pi1 * Mpg[3 + jj]) + pi2 * Mpg[6 + jj];
+          Gv[jj] = (g == pv) ? sel3(jj, pi0, pi1, pi2) : pr;
+        }
+      } else {
+        double W[3];
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) W[jj] = (gi[0] * Pinv[jj] + gi[1] * Pinv[3 + jj]) + gi[2] * Pinv[6 + jj];
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+          const double up = Gv[jj] - ((W[0] * Mpg[jj] + W[1] * Mpg[3 + jj]) + W[2] * Mpg[6 + jj]);
+          Gv[jj] = (g == pv) ? -W[jj] : up;
+        }
+      }
     }
+    if (act)
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) F.Gi[k][12 * i + 3 * g + jj] = Gv[jj];
     wave_sync();
     if (k >= 1) {
-      for (int e = t; e < 144; e += NT) {  // K_k = G^-1 F
-        const int i = e / 12, j = e % 12;
-        double s = 0.0;
-        for (int q = 0; q < 12; ++q) s += F.Gi[k][i * 12 + q] * F.F[q * 12 + j];
-        F.K[k][e] = s;
+      // F = B_k' P A
+      double Fv[3];
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) {
+        const int cc = 3 * g + jj;
+        Fv[jj] = ((bi0 * F.PA[72 + cc] + bi1 * F.PA[84 + cc]) + bi2 * F.PA[96 + cc]) + dtm * F.PA[12 * si + cc];
       }
+      if (act)
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) F.F[12 * i + 3 * g + jj] = Fv[jj];
       wave_sync();
-      for (int e = t; e < 144; e += NT) {  // Acl_k = A - B_k K_k, P_k = cQ + A'PA - F'K_k
-        const int i = e / 12, j = e % 12;
+      // K_k = G^-1 F
+      double gr[12];
+      ld12(gr, &F.Gi[k][12 * i]);
+      double Kv[3];
+#pragma unroll 1
+      for (int jj = 0; jj < 3; ++jj) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) s += gr[q] * F.F[12 * q + 3 * g + jj];
+        Kv[jj] = s;
+      }
+      double* Kk = F.K[k - 1];
+      if (act)
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) Kk[12 * i + 3 * g + jj] = Kv[jj];
+      wave_sync();
+      // Acl_k = A - B_k K_k ; P_k = cQ + A'(PA) - F' K_k
+#pragma unroll 1
+      for (int jj = 0; jj < 3; ++jj) {
+        const int cc = 3 * g + jj;
         double bk = 0.0;
         if (i >= 6 && i < 9) {
-          for (int q = 0; q < 12; ++q) bk += sm.Bw[k][i - 6][q] * F.K[k][q * 12 + j];
+          const double* bw = sm.Bw[k][i - 6];
+#pragma unroll
+          for (int q = 0; q < 12; ++q) bk += bw[q] * Kk[12 * q + cc];
         } else if (i >= 9) {
-          const int a = i - 9;
-          bk = dtm * (((F.K[k][a * 12 + j] + F.K[k][(3 + a) * 12 + j]) + F.K[k][(6 + a) * 12 + j]) +
-                      F.K[k][(9 + a) * 12 + j]);
+          const int a3 = i - 9;
+          bk = dtm * (((Kk[12 * a3 + cc] + Kk[12 * (3 + a3) + cc]) + Kk[12 * (6 + a3) + cc]) + Kk[12 * (9 + a3) + cc]);
         }
-        if (k <= N - 2) F.Acl[k][e] = A.at(i, j) - bk;
         double fk = 0.0;
-        for (int q = 0; q < 12; ++q) fk += F.F[q * 12 + i] * F.K[k][q * 12 + j];
-        F.P[e] = (((i == j) ? c * (2.0 * p.q_weights[i]) : 0.0) + A.atm(F.PA, i, j)) - fk;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) fk += F.F[12 * q + i] * Kk[12 * q + cc];
+        const double pn = (((i == cc) ? c * (2.0 * p.q_weights[i]) : 0.0) + A.atm(F.PA, i, cc)) - fk;
+        if (act) {
+          if (k <= N - 2) F.Acl[k - 1][12 * i + cc] = A.at(i, cc) - bk;
+          F.P[12 * i + cc] = pn;
+        }
       }
       wave_sync();
     }
@@ -355,7 +487,7 @@ __device__ void factorize(WSmem<N>& sm, const mpcqp_params& p, const Adisc& A, d
 #endif
 
 template <int N>
-__global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ recs, int batch,
+__global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ recs, int batch,
                                                      mpcqp_result* __restrict__ results,
                                                      double* __restrict__ solution, double* __restrict__ trace,
                                                      int trace_cap, mpcqp_params p) {
@@ -375,12 +507,13 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
   WV_MARK(0);
 
   // ---- 0. record -> LDS, non-finite guard -------------------------------------------------------
+  auto& HS = sm.u.h;
   {
     const double* rg = recs + (size_t)inst * C::REC;
     bool bad = false;
     for (int e = t; e < C::REC; e += NT) {
       const double v = rg[e];
-      sm.rec[e] = v;
+      HS.rec[e] = v;
       bad |= !isfinite(v);
     }
     if (__ballot(bad) != 0) {
@@ -398,7 +531,7 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
   }
   wave_sync();
   WV_MARK(1);
-  const double* rec = sm.rec;
+  const double* rec = HS.rec;
   const double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS], mu = rec[MPCQP_REC_MU];
   Adisc A;
   {
@@ -408,6 +541,12 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
     A.dt = dt;
   }
   const double dtm = (1.0 / mass) * dt;
+  // what the solve needs from the record after the setup image is recycled
+  double Rot[9];
+#pragma unroll
+  for (int e = 0; e < 9; ++e) Rot[e] = rec[MPCQP_REC_ROT + e];
+  const double cont = rec[MPCQP_REC_CONTACTS + leg] != 0.0 ? 1.0 : 0.0;
+  const double fzmin = rec[MPCQP_REC_FZMIN], fzmax = rec[MPCQP_REC_FZMAX];
 
   // ---- 1. B_d(k) rows 6-8 (calculate_B_mat_c, Utils.cpp:35-41), gradient adjoint --------------------
   {
@@ -427,11 +566,11 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
       sm.Bw[k][rr][cc] = s * dt;
     }
     // forward: a_i = A_d^{i+1} x0 (13 states), e_i = 2q (a_i - x_ref_i) (ConvexMpc.cpp:215-217)
-    if (t < SD) sm.vec[0][t] = rec[MPCQP_REC_X0 + t];
+    if (t < SD) HS.vec[0][t] = rec[MPCQP_REC_X0 + t];
     wave_sync();
     for (int i = 0; i < N; ++i) {
       if (t < SD) {
-        const double* pv = sm.vec[i & 1];
+        const double* pv = HS.vec[i & 1];
         double s;
         if (t == 0) s = (pv[0] + A.ad0 * pv[6]) + A.ad1 * pv[7];
         else if (t == 1) s = (pv[1] + (-A.ad1) * pv[6]) + A.ad0 * pv[7];
@@ -439,119 +578,168 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
         else if (t <= 5) s = pv[t] + dt * pv[t + 6];
         else if (t == 11) s = pv[11] + dt * pv[12];
         else s = pv[t];
-        sm.vec[(i + 1) & 1][t] = s;
-        if (t < ND) sm.lam[i][t] = 2 * p.q_weights[t] * (s - rec[MPCQP_REC_XREF + SD * i + t]);
+        HS.vec[(i + 1) & 1][t] = s;
+        if (t < ND) HS.lam[i][t] = 2 * p.q_weights[t] * (s - rec[MPCQP_REC_XREF + SD * i + t]);
       }
       wave_sync();
     }
     // backward: lambda_j = e_j + A' lambda_{j+1}
     for (int j = N - 2; j >= 0; --j) {
-      if (t < ND) sm.lam[j][t] = sm.lam[j][t] + A.atv(t, sm.lam[j + 1]);
+      if (t < ND) HS.lam[j][t] = HS.lam[j][t] + A.atv(t, HS.lam[j + 1]);
       wave_sync();
     }
   }
-
   WV_MARK(2);
-  // ---- 2. |H| (fp32, packed) from H_jk = B_j' (A')^{k-j} S_k B_k (+ R on the diagonal) -------------
-  auto& HS = sm.u.h;
-  for (int e = t; e < 144; e += NT) {
-    const int i = e / 12, j = e % 12;
-    HS.S[e] = (i == j) ? 2 * p.q_weights[i] : 0.0;
-  }
-  wave_sync();
-  for (int k = N - 1; k >= 0; --k) {
-    for (int e = t; e < 144; e += NT) HS.G[k][e] = mb(sm, HS.S, k, e / 12, e % 12, dtm);  // G_k = S_k B_k
-    if (k >= 1) {
-      for (int e = t; e < 144; e += NT) HS.T[e] = A.ma(HS.S, e / 12, e % 12);
-      wave_sync();
-      for (int e = t; e < 144; e += NT) {
-        const int i = e / 12, j = e % 12;
-        HS.S[e] = ((i == j) ? 2 * p.q_weights[i] : 0.0) + A.atm(HS.T, i, j);
-      }
-    }
-    wave_sync();
-  }
-  for (int k = 0; k < N; ++k) {
-    const double* V = HS.G[k];  // V_{j,k} = (A')^{k-j} G_k, double-buffered
-    int wb = 0;
-    for (int j = k; j >= 0; --j) {
-      for (int e = t; e < 144; e += NT) {
-        const int b = e / 12, aa = e % 12;
-        double h = btm(sm, V, j, b, aa, dtm);
-        if (j == k && b == aa) h += 2 * p.r_weights[b];
-        const int row = ND * j + b, col = ND * k + aa;
-        if (row <= col) HS.H32[hidx(row, col)] = (float)dabs(h);
-        if (j > 0) HS.V[wb][e] = A.atm(V, b, aa);
-      }
-      wave_sync();
-      V = HS.V[wb];
-      wb ^= 1;
-    }
-  }
 
   WV_MARK(3);
+
   // ---- 3. OSQP scale_data (scaling.c) with the scaling deferred: P~ = c D H D is never formed -------
-  // Column inf-norms of P~ are (c D_j) max_i D_i |H_ij| (H symmetric), from the fp32 |H|.
+  // Column inf-norms of P~ are (c D_j) max_i D_i |H_ij| (H symmetric).  H is never stored either:
+  // every pass regenerates the lane's columns c = t, t + 64 of H = B'Q̄B + R in binary64.  A_c is
+  // nilpotent on the 12 moving states (A_c^2 = 0), so A^m = I + m Ac (Ac := dt A_c) and
+  //   S_j = sum_{m=0}^{M_j} (A^m)' Q A^m = (M_j+1) Q + T1_j (Q Ac + Ac'Q) + T2_j Ac'Q Ac,
+  //   M_j = N-1-j, T1 = M(M+1)/2, T2 = M(M+1)(2M+1)/6.  With y = B_k e_a (column c = 12k + a):
+  //   block j <= k:  H_jk e_a = B_j' (A')^{k-j} S_k y = B_j' (g + (k-j) Ac'g),   g = S_k y
+  //   block j >  k:  H_jk e_a = B_j' S_j A^{j-k} y   = B_j' S_j (y + (j-k) Ac y)
+  // and only rows 6-11 of the 12-vector inside B_j' matter.  A~ = E A D entries are E_r |A_rj| D_j
+  // (A: ConvexMpc.cpp:46-58, entries 1 and +-mu).
   for (int j = t; j < n; j += NT) {
     const int k = j / ND, ii = j % ND;
-    const double* lm = sm.lam[k];
+    const double* lm = HS.lam[k];
     HS.q[j] = ((sm.Bw[k][0][ii] * lm[6] + sm.Bw[k][1][ii] * lm[7]) + sm.Bw[k][2][ii] * lm[8]) + dtm * lm[9 + ii % 3];
     HS.D[j] = 1.0;
-    HS.D32[j] = 1.0f;
   }
-  for (int r = t; r < m; r += NT) {  // unscaled A rows (ConvexMpc.cpp:46-58)
-    const int k5 = r % 5;
-    const double az = k5 == 4 ? 0.0 : ((k5 & 1) ? -mu : mu);
-    HS.ak[r][0] = k5 < 2 ? 1.0 : 0.0;
-    HS.ak[r][1] = (k5 == 2 || k5 == 3) ? 1.0 : 0.0;
-    HS.ak[r][2] = k5 < 4 ? az : 1.0;
-    HS.E[r] = 1.0;
-  }
+  for (int r = t; r < m; r += NT) HS.E[r] = 1.0;
   wave_sync();
-  auto colmax = [&]() __attribute__((always_inline)) {
-    for (int j = t; j < n; j += NT) {
-      float mx = 0.0f;
-      for (int i = 0; i < n; ++i) {
-        const float h = HS.H32[i <= j ? hidx(i, j) : hidx(j, i)];
-        mx = fmaxf(mx, HS.D32[i] * h);
+  const double amu = dabs(mu);
+  auto colmax1 = [&](int c) __attribute__((always_inline)) -> double {  // max_i D_i |H_ic|
+    const int k = c / ND, a2 = c % ND;
+    double y[12], w[12];
+#pragma unroll
+    for (int s2 = 0; s2 < 12; ++s2) y[s2] = 0.0;
+    y[6] = sm.Bw[k][0][a2];
+    y[7] = sm.Bw[k][1][a2];
+    y[8] = sm.Bw[k][2][a2];
+    y[9 + a2 % 3] = dtm;
+    w[0] = A.ad0 * y[6] + A.ad1 * y[7];
+    w[1] = (-A.ad1) * y[6] + A.ad0 * y[7];
+    w[2] = dt * y[8];
+    w[3] = dt * y[9];
+    w[4] = dt * y[10];
+    w[5] = dt * y[11];
+#pragma unroll
+    for (int s2 = 6; s2 < 12; ++s2) w[s2] = 0.0;
+    double qy[12], qw[12];
+#pragma unroll
+    for (int s2 = 0; s2 < 12; ++s2) {
+      qy[s2] = 2 * p.q_weights[s2] * y[s2];
+      qw[s2] = 2 * p.q_weights[s2] * w[s2];
+    }
+    auto actv = [&](const double (&v)[12], double (&o)[6]) __attribute__((always_inline)) {
+      o[0] = A.ad0 * v[0] + (-A.ad1) * v[1];
+      o[1] = A.ad1 * v[0] + A.ad0 * v[1];
+      o[2] = dt * v[2];
+      o[3] = dt * v[3];
+      o[4] = dt * v[4];
+      o[5] = dt * v[5];
+    };
+    double u1[6], u2[6];
+    actv(qy, u1);
+    actv(qw, u2);
+    const double Mk = (double)(N - 1 - k);
+    const double T1k = Mk * (Mk + 1) / 2, T2k = Mk * (Mk + 1) * (2 * Mk + 1) / 6;
+    double g[12];
+#pragma unroll
+    for (int s2 = 0; s2 < 12; ++s2) {
+      const double ac = s2 >= 6 ? u1[s2 - 6] : 0.0, ac2 = s2 >= 6 ? u2[s2 - 6] : 0.0;
+      g[s2] = ((Mk + 1) * qy[s2] + T1k * (qw[s2] + ac)) + T2k * ac2;
+    }
+    double h[6];
+    actv(g, h);
+    double mx0 = 0.0, mx1 = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < N; ++j) {
+      const bool up = j <= k;
+      const double d = (double)(j - k);
+      const double Mj = (double)(N - 1 - j);
+      const double T1j = Mj * (Mj + 1) / 2, T2j = Mj * (Mj + 1) * (2 * Mj + 1) / 6;
+      const double cg = up ? 1.0 : 0.0, ch = up ? -d : 0.0;
+      const double cqy = up ? 0.0 : Mj + 1, cqw = up ? 0.0 : (Mj + 1) * d + T1j;
+      const double cu1 = up ? 0.0 : T1j, cu2 = up ? 0.0 : T1j * d + T2j;
+      double v[6];
+#pragma unroll
+      for (int s2 = 0; s2 < 6; ++s2)
+        v[s2] = ((((cg * g[6 + s2] + ch * h[s2]) + cqy * qy[6 + s2]) + cqw * qw[6 + s2]) + cu1 * u1[s2]) + cu2 * u2[s2];
+      const double* bw0 = sm.Bw[j][0];
+      const double* bw1 = sm.Bw[j][1];
+      const double* bw2 = sm.Bw[j][2];
+      const double* dj = HS.D + ND * j;
+#pragma unroll
+      for (int b = 0; b < 12; ++b) {
+        double hv = ((bw0[b] * v[0] + bw1[b] * v[1]) + bw2[b] * v[2]) + dtm * v[3 + b % 3];
+        if (j == k && b == a2) hv += 2 * p.r_weights[b];
+        if (b & 1) mx1 = fmax(mx1, dj[b] * dabs(hv));
+        else mx0 = fmax(mx0, dj[b] * dabs(hv));
       }
-      HS.cm[j] = (double)mx;
     }
+    return fmax(mx0, mx1);
   };
-  double c_s = 1.0;
-  if (p.scaling > 0) {
-    colmax();
-    wave_sync();
-  }
+  auto colmax = [&](double& cm0, double& cm1) __attribute__((always_inline)) {
+    cm0 = colmax1(t);
+    cm1 = t + 64 < n ? colmax1(t + 64) : 0.0;
+  };
+  // column norm of A~ for variable j / row norm of A~ for row r
+  auto acol = [&](int j) __attribute__((always_inline)) {
+    const int f = j / 3, aa = j % 3;
+    const double* e = HS.E + 5 * f;
+    double mx;
+    if (aa == 0) mx = dmax(e[0], e[1]);
+    else if (aa == 1) mx = dmax(e[2], e[3]);
+    else mx = dmax(dmax(dmax(dmax(amu * e[0], amu * e[1]), amu * e[2]), amu * e[3]), e[4]);
+    return mx * HS.D[j];
+  };
+  auto arow = [&](int r) __attribute__((always_inline)) {
+    const int f = r / 5, k5 = r % 5;
+    const double e = HS.E[r];
+    const double* d = HS.D + 3 * f;
+    if (k5 == 4) return e * d[2];
+    return dmax(e * d[k5 >> 1], (amu * e) * d[2]);
+  };
+  double c_s = 1.0, cm0 = 0.0, cm1 = 0.0;
+  if (p.scaling > 0) colmax(cm0, cm1);
   for (int pass = 0; pass < p.scaling; ++pass) {
-    for (int j = t; j < n; j += NT) {
-      const int f = j / 3, aa = j % 3;
-      double ca = 0.0;
-      for (int k = 0; k < 5; ++k) ca = fmax(ca, dabs(HS.ak[5 * f + k][aa]));
-      const double pc = (c_s * HS.D[j]) * HS.cm[j];
-      HS.Dt[j] = 1.0 / sqrt(limit_scaling(fmax(pc, ca)));
+    for (int half = 0; half < 2; ++half) {
+      const int j = t + 64 * half;
+      if (j < n) {
+        const double pc = (c_s * HS.D[j]) * (half ? cm1 : cm0);
+        HS.Dt[j] = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j))));
+      }
+    }
+    double et[(C::m + NT - 1) / NT];
+#pragma unroll
+    for (int rr = 0; rr < (C::m + NT - 1) / NT; ++rr) {
+      const int r = t + NT * rr;
+      et[rr] = r < m ? 1.0 / sqrt(limit_scaling(arow(r))) : 1.0;
     }
     wave_sync();
-    for (int r = t; r < m; r += NT) {  // A <- E A D
-      const int f = r / 5;
-      const double et =
-          1.0 / sqrt(limit_scaling(fmax(fmax(dabs(HS.ak[r][0]), dabs(HS.ak[r][1])), dabs(HS.ak[r][2]))));
-      HS.ak[r][0] = (HS.ak[r][0] * et) * HS.Dt[3 * f];
-      HS.ak[r][1] = (HS.ak[r][1] * et) * HS.Dt[3 * f + 1];
-      HS.ak[r][2] = (HS.ak[r][2] * et) * HS.Dt[3 * f + 2];
-      HS.E[r] *= et;
+#pragma unroll
+    for (int rr = 0; rr < (C::m + NT - 1) / NT; ++rr) {
+      const int r = t + NT * rr;
+      if (r < m) HS.E[r] *= et[rr];
     }
     for (int j = t; j < n; j += NT) {
       HS.q[j] = HS.Dt[j] * HS.q[j];
       HS.D[j] = HS.D[j] * HS.Dt[j];
-      HS.D32[j] = (float)HS.D[j];
     }
     wave_sync();
-    colmax();  // column norms of the D-scaled P (cost normalization)
+    colmax(cm0, cm1);  // column norms of the D-scaled P (cost normalization)
     double sv = 0.0, qv = 0.0;
-    for (int j = t; j < n; j += NT) {
-      sv += (c_s * HS.D[j]) * HS.cm[j];
-      qv = fmax(qv, dabs(HS.q[j]));
+    for (int half = 0; half < 2; ++half) {
+      const int j = t + 64 * half;
+      if (j < n) {
+        sv += (c_s * HS.D[j]) * (half ? cm1 : cm0);
+        qv = fmax(qv, dabs(HS.q[j]));
+      }
     }
     sv = wave_sum(sv);
     qv = wave_max(qv);
@@ -573,7 +761,6 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
   double Z[R], Y[R], DY[R], Ev[R], AK0[R], AK1[R];
   double Z4[R], Y4[R], DY4[R], E4[R], L4[R], U4[R], AK4[R], RHO4[R];
   bool kvr[R], vvr[R];
-  const double cont = rec[MPCQP_REC_CONTACTS + leg] != 0.0 ? 1.0 : 0.0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int k = 4 * r + ig;
@@ -582,16 +769,18 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
     vvr[r] = vv;
     const int kc = kv ? k : 0;
     const int ci = ND * kc + idx, ri = CD * kc + 5 * leg + a, r4 = CD * kc + 5 * leg + 4;
+    const int cf = ND * kc + 3 * leg;  // the leg's three variables
     Dv[r] = vv ? HS.D[ci] : 1.0;
     DI[r] = 1. / Dv[r];
     Qv[r] = vv ? HS.q[ci] : 0.0;
     Ev[r] = kv ? HS.E[ri] : 1.0;
     E4[r] = kv ? HS.E[r4] : 1.0;
-    AK0[r] = kv ? HS.ak[ri][a >> 1] : 0.0;
-    AK1[r] = kv ? HS.ak[ri][2] : 0.0;
-    AK4[r] = kv ? HS.ak[r4][2] : 0.0;
+    // A~ = E A D: row a < 4 has 1 on fx (a < 2) / fy (a >= 2) and +-mu on fz; row 4 has 1 on fz
+    AK0[r] = kv ? Ev[r] * HS.D[cf + (a >> 1)] : 0.0;
+    AK1[r] = kv ? (((a & 1) ? -mu : mu) * Ev[r]) * HS.D[cf + 2] : 0.0;
+    AK4[r] = kv ? E4[r] * HS.D[cf + 2] : 0.0;
     // bounds (ConvexMpc.cpp:223-245), clipped to +-OSQP_INFTY, scaled by E
-    double l4 = rec[MPCQP_REC_FZMIN] * cont, u4 = rec[MPCQP_REC_FZMAX] * cont;
+    double l4 = fzmin * cont, u4 = fzmax * cont;
     l4 = dmin(dmax(l4, -OSQP_INF), OSQP_INF);
     u4 = dmin(dmax(u4, -OSQP_INF), OSQP_INF);
     L4[r] = E4[r] * l4;
@@ -648,7 +837,7 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
           const double db = b == 0 ? d0 : (b == 1 ? d1 : d2);
           const double rt = (av && a == b ? cost_c * (2.0 * p.r_weights[idx]) : 0.0) +
                             ((1.0 / da) * ((av && a == b ? sigma : 0.0) + s)) * (1.0 / db);
-          if (kvr[r] && av) F.Rt[k][idx][b] = rt;
+          if (kvr[r] && av && b >= a) F.Rt[k][leg][sym6(a, b)] = rt;
         }
       }
       wave_sync();
@@ -663,77 +852,90 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
     const bool tm_it = iter == 60;
     if (tm_it) WV_MARK(40);
     {
-      double W[R], AKw[R], BKw[R], SMv[R], G[R], Hh[R], XS[R];
+      double W[R], AKw[R], SMv[R], G[R], Hh[R], XS[R], c[R][12];
+      int kc[R], kk[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         W[r] = DI[r] * RHS[r];
         SMv[r] = 0.0;
         XS[r] = 0.0;
+        kc[r] = min(4 * r + ig, N - 1);
+        kk[r] = max(kc[r] - 1, 0);  // slot of K_k (k >= 1)
       }
+      // a_k = K_k' w_k (k >= 1)
 #pragma unroll
-      for (int r = 0; r < R; ++r) {  // a_k = K_k' w_k, b_k = G_k^-1 w_k
-        const int kc = min(4 * r + ig, N - 1);
-        double c[12];
-        ld12s(c, &F.K[kc][idx]);
-        AKw[r] = mv12(W[r], c);
-        ld12(c, &F.Gi[kc][12 * idx]);
-        BKw[r] = mv12(W[r], c);
-      }
+      for (int r = 0; r < R; ++r) ld12s(c[r], &F.K[kk[r]][idx]);
+      mv_rounds<R>(W, c, AKw);
       if (tm_it) WV_MARK(41);
       {  // backward chain: s_{N-1} = -a_{N-1}; s_k = Acl_k' s_{k+1} - a_k; SMv (row of k) = s_{k+1}
         double cur = -AKw[(N - 1) >> 2];
+        double cn[12];
+        if constexpr (N >= 3) ld12s(cn, &F.Acl[N - 3][idx]);
         sfor<0, N - 1>([&](auto J) {
           constexpr int k = N - 2 - decltype(J)::value;
           const double mvv = rmove<row_of(k + 1), row_of(k)>(cur);
           SMv[k >> 2] = (q == row_of(k)) ? mvv : SMv[k >> 2];
           if constexpr (k >= 1) {
-            double c[12];
-            ld12s(c, &F.Acl[k][idx]);
-            cur = mv12(mvv, c) - AKw[k >> 2];
+            double cc[12];
+#pragma unroll
+            for (int e = 0; e < 12; ++e) cc[e] = cn[e];
+            if constexpr (k >= 2) ld12s(cn, &F.Acl[k - 2][idx]);  // prefetch the next step's column
+            cur = mv12(mvv, cc) - AKw[k >> 2];
           }
         });
       }
       if (tm_it) WV_MARK(42);
+      // g_k = G_k^-1 (w_k + B_k' s_{k+1})
+      {
+        double tt[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {  // g_k = b_k + G_k^-1 B_k' s_{k+1}; h_k = B_k g_k
-        const int kc = min(4 * r + ig, N - 1);
-        const double c6[6] = {sm.Bw[kc][0][idx], sm.Bw[kc][1][idx], sm.Bw[kc][2][idx],
-                              a == 0 ? dtm : 0.0, a == 1 ? dtm : 0.0, a == 2 ? dtm : 0.0};
-        const double tt = mv6(SMv[r], c6);
-        double c[12];
-        ld12(c, &F.Gi[kc][12 * idx]);
-        G[r] = BKw[r] + mv12(tt, c);
-        ld12(c, &sm.Bw[kc][av ? a : 2][0]);
-#pragma unroll
-        for (int cc = 0; cc < 12; ++cc)
-          c[cc] = (leg == 2 && av) ? c[cc] : ((leg == 3 && av && cc % 3 == a) ? dtm : 0.0);
-        Hh[r] = mv12(G[r], c);
+        for (int r = 0; r < R; ++r) {
+          const double c6[6] = {sm.Bw[kc[r]][0][idx], sm.Bw[kc[r]][1][idx], sm.Bw[kc[r]][2][idx],
+                                a == 0 ? dtm : 0.0, a == 1 ? dtm : 0.0, a == 2 ? dtm : 0.0};
+          tt[r] = W[r] + mv6(SMv[r], c6);
+          ld12(c[r], &F.Gi[kc[r]][12 * idx]);
+        }
+        mv_rounds<R>(tt, c, G);
       }
+      // h_k = B_k g_k (rows 6-8: B_w, rows 9-11: dt/m on the matching force component)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        ld12(c[r], &sm.Bw[kc[r]][av ? a : 2][0]);
+#pragma unroll
+        for (int e = 0; e < 12; ++e)
+          c[r][e] = (leg == 2 && av) ? c[r][e] : ((leg == 3 && av && e % 3 == a) ? dtm : 0.0);
+      }
+      mv_rounds<R>(G, c, Hh);
       if (tm_it) WV_MARK(43);
       {  // forward chain: x_1 = h_0; x_{k+1} = Acl_k x_k + h_k; XS (row of k) = x_k
         double cur = Hh[0];
+        double cn[12];
+        if constexpr (N >= 3) ld12(cn, &F.Acl[0][12 * idx]);
         sfor<1, N>([&](auto K) {
           constexpr int k = decltype(K)::value;
           const double mvv = rmove<row_of(k - 1), row_of(k)>(cur);
           XS[k >> 2] = (q == row_of(k)) ? mvv : XS[k >> 2];
           if constexpr (k <= N - 2) {
-            double c[12];
-            ld12(c, &F.Acl[k][12 * idx]);
-            cur = mv12(mvv, c) + Hh[k >> 2];
+            double cc[12];
+#pragma unroll
+            for (int e = 0; e < 12; ++e) cc[e] = cn[e];
+            if constexpr (k + 1 <= N - 2) ld12(cn, &F.Acl[k][12 * idx]);  // prefetch
+            cur = mv12(mvv, cc) + Hh[k >> 2];
           }
         });
       }
       if (tm_it) WV_MARK(44);
+      // u_k = g_k - K_k x_k (x_0 = 0)
+      {
+        double kx[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {  // u_k = g_k - K_k x_k
-        const int kc = min(4 * r + ig, N - 1);
-        double c[12];
-        ld12(c, &F.K[kc][12 * idx]);
-        U[r] = G[r] - mv12(XS[r], c);
+        for (int r = 0; r < R; ++r) ld12(c[r], &F.K[kk[r]][12 * idx]);
+        mv_rounds<R>(XS, c, kx);
+#pragma unroll
+        for (int r = 0; r < R; ++r) U[r] = G[r] - kx[r];
       }
     }
     if (tm_it) WV_MARK(45);
-
     bool is_check = false, is_adapt = false;
     if (p.check_termination && --to_check == 0) {
       is_check = true;
@@ -985,11 +1187,10 @@ __global__ __launch_bounds__(NT, 2) void wave_kernel(const double* __restrict__ 
   const bool nanleg = isnan(nrm);
   const unsigned long long nanmask = __ballot(q == 0 && a == 0 && nanleg);
   if (q == 0 && av) {
-    const double* Rm = rec + MPCQP_REC_ROT;
     double s = 0.0;
-    s += Rm[0 * 3 + a] * u00;
-    s += Rm[1 * 3 + a] * u01;
-    s += Rm[2 * 3 + a] * u02;
+    s += sel3(a, Rot[0], Rot[1], Rot[2]) * u00;
+    s += sel3(a, Rot[3], Rot[4], Rot[5]) * u01;
+    s += sel3(a, Rot[6], Rot[7], Rot[8]) * u02;
     res->u0[3 * leg + a] = xs0;
     res->f_body[3 * leg + a] = nanleg ? 0.0 : s;
   }
