@@ -171,6 +171,9 @@ def main():
                     f"{args.gait} gait{', mu~U(0.3,0.9)' if args.mixed_mu else ''}; "
                     f"cold-start OSQP-0.6 settings, adaptive-rho interval 25")
         key = f"N{N}_B{B}_{args.gait}{'_mu' if args.mixed_mu else ''}"
+        eff = path or 3
+        kernel_name = {1: f"mpcqp::solve_kernel<{N}>", 2: f"mpcqp::ric::ric_solve_kernel<{N}>",
+                       3: f"mpcqp::wv::wave_kernel<{N}>"}[eff]
         traffic = load_traffic(key)
         out = {
             "metric": METRIC,
@@ -191,7 +194,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS,
                          "traffic": traffic,
-                         "kernel": f"mpcqp::solve_kernel<{N}>", "kernel_ms": kern_ms,
+                         "kernel": kernel_name, "kernel_ms": kern_ms,
                          "algorithmic_flop_per_launch": flops,
                          "note": "binary64 VALU-bound; peak = FP64 vector (=FP64 MFMA) spec"},
             "cpu_baseline": cpu,

@@ -56,7 +56,7 @@ bool params_valid(const mpcqp_params* p) {
 // 1 dense K^-1, 2 Riccati (one workgroup per robot), 3 Riccati (one wave per robot)
 int effective_path(const mpcqp_handle* h) {
   if (h->path != 0) return h->path;
-  return h->p.horizon > mpcqp::DENSE_MAX_HORIZON ? 2 : 1;
+  return h->p.horizon <= mpcqp::WAVE_MAX_HORIZON ? 3 : 2;
 }
 size_t work_per_instance(const mpcqp_handle* h) {
   switch (effective_path(h)) {
@@ -299,7 +299,7 @@ int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {
 }
 int32_t mpcqp_solve_threads(int32_t horizon) {
   if (horizon < 1 || horizon > MPCQP_MAX_HORIZON) return 0;
-  return horizon > mpcqp::DENSE_MAX_HORIZON ? mpcqp::riccati_threads(horizon) : mpcqp::solve_threads(horizon);
+  return horizon <= mpcqp::WAVE_MAX_HORIZON ? 64 : mpcqp::riccati_threads(horizon);
 }
 
 int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {

@@ -39,6 +39,6 @@ constexpr int DENSE_MAX_HORIZON = 10;
 hipError_t launch_wave_any(const LaunchArgs& a);
 hipError_t occupancy_wave_any(int horizon, int* blocks);
 hipError_t wave_selftest(double* d_out, void* stream);
-constexpr int WAVE_MAX_HORIZON = 10;
+constexpr int WAVE_MAX_HORIZON = 20;
 
 }  // namespace mpcqp

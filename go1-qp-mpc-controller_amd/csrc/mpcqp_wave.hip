@@ -684,9 +684,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     }
     return fmax(mx0, mx1);
   };
-  auto colmax = [&](double& cm0, double& cm1) __attribute__((always_inline)) {
-    cm0 = colmax1(t);
-    cm1 = t + 64 < n ? colmax1(t + 64) : 0.0;
+  constexpr int NC = (C::n + NT - 1) / NT;  // columns per lane: t, t + 64, ...
+  auto colmax = [&](double (&cm)[NC]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < NC; ++h) cm[h] = t + NT * h < n ? colmax1(t + NT * h) : 0.0;
   };
   // column norm of A~ for variable j / row norm of A~ for row r
   auto acol = [&](int j) __attribute__((always_inline)) {
@@ -705,13 +706,16 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     if (k5 == 4) return e * d[2];
     return dmax(e * d[k5 >> 1], (amu * e) * d[2]);
   };
-  double c_s = 1.0, cm0 = 0.0, cm1 = 0.0;
-  if (p.scaling > 0) colmax(cm0, cm1);
+  double c_s = 1.0, cm[NC];
+#pragma unroll
+  for (int h = 0; h < NC; ++h) cm[h] = 0.0;
+  if (p.scaling > 0) colmax(cm);
   for (int pass = 0; pass < p.scaling; ++pass) {
-    for (int half = 0; half < 2; ++half) {
-      const int j = t + 64 * half;
+#pragma unroll
+    for (int h = 0; h < NC; ++h) {
+      const int j = t + NT * h;
       if (j < n) {
-        const double pc = (c_s * HS.D[j]) * (half ? cm1 : cm0);
+        const double pc = (c_s * HS.D[j]) * cm[h];
         HS.Dt[j] = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j))));
       }
     }
@@ -732,12 +736,13 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       HS.D[j] = HS.D[j] * HS.Dt[j];
     }
     wave_sync();
-    colmax(cm0, cm1);  // column norms of the D-scaled P (cost normalization)
+    colmax(cm);  // column norms of the D-scaled P (cost normalization)
     double sv = 0.0, qv = 0.0;
-    for (int half = 0; half < 2; ++half) {
-      const int j = t + 64 * half;
+#pragma unroll
+    for (int h = 0; h < NC; ++h) {
+      const int j = t + NT * h;
       if (j < n) {
-        sv += (c_s * HS.D[j]) * (half ? cm1 : cm0);
+        sv += (c_s * HS.D[j]) * cm[h];
         qv = fmax(qv, dabs(HS.q[j]));
       }
     }
@@ -1240,7 +1245,8 @@ static hipError_t occupancy_wave(int* blocks) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wv::wave_kernel<N>, wv::NT, 0);
 }
 
-#define MPCQP_WAVE_FOR_EACH_N(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10)
+#define MPCQP_WAVE_FOR_EACH_N(X) \
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20)
 
 hipError_t launch_wave_any(const LaunchArgs& a) {
   switch (a.p.horizon) {

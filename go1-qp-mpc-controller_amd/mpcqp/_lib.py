@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(PKG_ROOT, "lib", "libmpcq
 
 STATE_DIM, NUM_LEG, NUM_DOF, CONSTRAINT_DIM = 13, 4, 12, 20
 MAX_HORIZON = 20
-DENSE_MAX_HORIZON = 10  # horizons above run the Riccati path
+DENSE_MAX_HORIZON = 10  # the dense K^-1 path (debug selection) serves horizons up to this
 SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI, SOLVER_WAVE = 0, 1, 2, 3
 OSQP_INFTY = 1e30
 

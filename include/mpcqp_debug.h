@@ -28,8 +28,8 @@ int32_t mpcqp_handle_slots(mpcqp_handle* h);
 /* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */
 int32_t mpcqp_solve_threads(int32_t horizon);
 
-/* Select the linear-system path of a handle: 0 auto, 1 dense K^-1 (N <= 10), 2 Riccati with
- * one workgroup per robot (any N), 3 Riccati with one wavefront per robot (N <= 10).  All paths
+/* Select the linear-system path of a handle: 0 auto (= 3), 1 dense K^-1 (N <= 10), 2 Riccati
+ * with one workgroup per robot, 3 Riccati with one wavefront per robot (the default).  All paths
  * run the same OSQP iteration; the selection exists to cross-check them on the same inputs. */
 int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path);
 
