@@ -43,15 +43,20 @@ def algorithmic_flops(N, iters, rho_updates):
                         + F_check * np.ceil(k / 25.0)))
 
 
-def load_traffic(config_key):
-    """Per-launch HBM bytes measured by a separate rocprofv3 --pmc pass (profiles/), or None."""
+def load_traffic(config_key, kernel):
+    """Per-launch HBM bytes of `kernel` measured by a separate rocprofv3 --pmc pass (profiles/),
+    or None when no pass of that kernel on this configuration is on file."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(config_key, {}).get("hbm_bytes_per_launch")
-    except Exception:
+            e = json.load(f).get(config_key, {})
+    except (OSError, ValueError):
         return None
+    short = kernel.split("::")[-1].split("<")[0]  # e.g. wave_kernel
+    tmpl = kernel[kernel.find("<"):] if "<" in kernel else ""
+    if short not in e.get("kernel", "") or tmpl not in e.get("kernel", ""):
+        return None
+    return e.get("hbm_bytes_per_launch")
 
 
 def main():
@@ -174,7 +179,7 @@ def main():
         eff = path or 3
         kernel_name = {1: f"mpcqp::solve_kernel<{N}>", 2: f"mpcqp::ric::ric_solve_kernel<{N}>",
                        3: f"mpcqp::wv::wave_kernel<{N}>"}[eff]
-        traffic = load_traffic(key)
+        traffic = load_traffic(key, kernel_name)
         out = {
             "metric": METRIC,
             "value": value,
