@@ -251,6 +251,16 @@ int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t 
   return MPCQP_OK;
 }
 
+int32_t mpcqp_joint_torques_device(const double* d_tq_records, const mpcqp_result* d_grf, int32_t batch,
+                                   int32_t* d_counter, double* d_joint_torques, void* stream) {
+  if (batch < 0 || (batch > 0 && (!d_tq_records || !d_grf || !d_counter || !d_joint_torques)))
+    return MPCQP_ERR_INVALID_ARG;
+  if (batch == 0) return MPCQP_OK;
+  return mpcqp::launch_torques(d_tq_records, d_grf, batch, d_counter, d_joint_torques, stream) == hipSuccess
+             ? MPCQP_OK
+             : MPCQP_ERR_HIP;
+}
+
 const char* mpcqp_status_str(int32_t s) {
   switch (s) {
     case MPCQP_STATUS_SOLVED: return "solved";

@@ -41,4 +41,8 @@ hipError_t occupancy_wave_any(int horizon, int* blocks);
 hipError_t wave_selftest(double* d_out, void* stream);
 constexpr int WAVE_MAX_HORIZON = 20;
 
+// Downstream torque map (mpcqp_torque.hip)
+hipError_t launch_torques(const double* recs, const mpcqp_result* grf, int batch, int* counter, double* tau,
+                          void* stream);
+
 }  // namespace mpcqp

@@ -10,9 +10,11 @@ from .records import (GO1_Q, GO1_R, RobotStates, assemble_compute_grf, assemble_
                       synthetic_go1)
 from .robot_control import Go1RobotControl, RobotControl
 from .solver import MpcQpSolver
+from .torques import assemble_torque_records, joint_torques_device
 
 __all__ = [
     "EXPORTED", "LIB_PATH", "RESULT_DTYPE", "MpcQpError", "Params", "Result", "default_params", "load",
     "rec_feet", "rec_size", "status_str", "GO1_Q", "GO1_R", "RobotStates", "assemble_compute_grf",
     "assemble_test_mpc", "synthetic_go1", "Go1RobotControl", "RobotControl", "MpcQpSolver",
+    "assemble_torque_records", "joint_torques_device",
 ]

@@ -24,6 +24,10 @@ REC_X0, REC_EULER, REC_ROT, REC_INERTIA = 0, 13, 16, 25
 REC_MASS, REC_MU, REC_FZMIN, REC_FZMAX, REC_DT, REC_CONTACTS, REC_XREF = 34, 35, 36, 37, 38, 39, 44
 
 
+# torque-map record layout (include/mpcqp.h MPCQP_TQ_*)
+TQ_JFOOT, TQ_FKIN, TQ_KM, TQ_GRAV, TQ_CONTACTS, TQ_SIZE = 0, 36, 48, 51, 63, 68
+
+
 def rec_feet(N):
     return REC_XREF + 13 * N
 
@@ -85,7 +89,7 @@ EXPORTED = [
     "mpcqp_solve_batch_device", "mpcqp_solve_batch_host", "mpcqp_build_qp_device",
     "mpcqp_status_str", "mpcqp_error_str", "mpcqp_last_error",
     "mpcqp_debug_solve_trace_device", "mpcqp_abi_sizes", "mpcqp_handle_slots", "mpcqp_solve_threads",
-    "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest",
+    "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_joint_torques_device",
 ]
 
 _lib = None
@@ -138,6 +142,8 @@ def load():
     L.mpcqp_debug_set_solver.restype = i32
     L.mpcqp_debug_wave_selftest.argtypes = [vp, vp]
     L.mpcqp_debug_wave_selftest.restype = i32
+    L.mpcqp_joint_torques_device.argtypes = [vp, vp, i32, vp, vp, vp]
+    L.mpcqp_joint_torques_device.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):

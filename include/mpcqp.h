@@ -153,6 +153,24 @@ int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t
 int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t batch,
                               double* d_P, double* d_q, double* d_l, double* d_u, void* stream);
 
+/* ---- downstream torque map: A1RobotControl::compute_joint_torques (A1RobotControl.cpp:289-319)
+ * One binary64 record per robot (offsets in doubles); FL, FR, RL, RR leg order.             */
+#define MPCQP_TQ_JFOOT 0      /* [4][9] j_foot.block<3,3>(3i,3i), row-major (A1CtrlStates.h:410) */
+#define MPCQP_TQ_FKIN 36      /* [4][3] foot_forces_kin column i (swing-leg PD force, :220-286)  */
+#define MPCQP_TQ_KM 48        /* [3]    km_foot                                                    */
+#define MPCQP_TQ_GRAV 51      /* [12]   torques_gravity                                            */
+#define MPCQP_TQ_CONTACTS 63  /* [4]    contacts[i] as 0.0 / 1.0                                   */
+#define MPCQP_TQ_SIZE 68      /* 67 used, padded to a multiple of 4 doubles                       */
+
+/* Replaces compute_joint_torques for `batch` robots (DEVICE pointers, async on `stream`):
+ *   d_counter[b] += 1 (mpc_init_counter); while it is < 10 the robot's torques are zeroed;
+ *   otherwise stance legs get tau = J^T (-f_grf), swing legs J tau = km .* f_kin (Eigen
+ *   PartialPivLU), plus torques_gravity, and non-NaN entries overwrite d_joint_torques[b][12].
+ * f_grf is taken from d_grf[b].f_body — the solve's output, so the MPC result never leaves the
+ * device (a NaN leg's f_body is 0 there; the reference leaves that column uninitialised). */
+int32_t mpcqp_joint_torques_device(const double* d_tq_records, const mpcqp_result* d_grf, int32_t batch,
+                                   int32_t* d_counter, double* d_joint_torques, void* stream);
+
 const char* mpcqp_status_str(int32_t status);
 const char* mpcqp_error_str(int32_t err);
 /* Last HIP error string recorded by the handle (for MPCQP_ERR_HIP). */

@@ -1354,6 +1354,77 @@ int32_t orc_solve_sequence(const mpcqp_params* prm, const double* recs, int32_t 
 }
 
 /* ============================================================================================
+ * Downstream torque map: A1RobotControl::compute_joint_torques (A1RobotControl.cpp:289-319)
+ * ========================================================================================== */
+
+/* Eigen PartialPivLU<Matrix3d>::solve: column-wise partial pivoting (first maximal |a_ik|,
+ * rows swapped whole), unit-lower forward and upper backward substitution. */
+static void lu3_solve(const double* J, const double* b, double* x) {
+  double a[9], y[3];
+  int perm[3] = {0, 1, 2};
+  memcpy(a, J, sizeof(a));
+  for (int k = 0; k < 3; ++k) {
+    int p = k;
+    double best = c_absval(a[3 * k + k]);
+    for (int i = k + 1; i < 3; ++i)
+      if (c_absval(a[3 * i + k]) > best) {
+        best = c_absval(a[3 * i + k]);
+        p = i;
+      }
+    if (p != k) {
+      for (int j = 0; j < 3; ++j) {
+        double t = a[3 * k + j];
+        a[3 * k + j] = a[3 * p + j];
+        a[3 * p + j] = t;
+      }
+      int t = perm[k];
+      perm[k] = perm[p];
+      perm[p] = t;
+    }
+    if (best != 0.0)
+      for (int i = k + 1; i < 3; ++i) a[3 * i + k] /= a[3 * k + k];
+    for (int i = k + 1; i < 3; ++i)
+      for (int j = k + 1; j < 3; ++j) a[3 * i + j] -= a[3 * i + k] * a[3 * k + j];
+  }
+  for (int i = 0; i < 3; ++i) y[i] = b[perm[i]];
+  for (int i = 1; i < 3; ++i)
+    for (int j = 0; j < i; ++j) y[i] -= a[3 * i + j] * y[j];
+  for (int i = 2; i >= 0; --i) {
+    double s = y[i];
+    for (int j = i + 1; j < 3; ++j) s -= a[3 * i + j] * x[j];
+    x[i] = s / a[3 * i + i];
+  }
+}
+
+void orc_joint_torques(const double* tq, const double* f_grf, int32_t* counter, double* tau) {
+  double jt[12];
+  *counter += 1;                 /* mpc_init_counter++ (:292) */
+  if (*counter < 10) {           /* first ticks: zero torques (:294-295) */
+    for (int k = 0; k < 12; ++k) tau[k] = 0.0;
+    return;
+  }
+  for (int leg = 0; leg < NL; ++leg) {
+    const double* J = tq + MPCQP_TQ_JFOOT + 9 * leg; /* j_foot.block<3,3>(3i,3i), row-major */
+    double* t = jt + 3 * leg;
+    if (tq[MPCQP_TQ_CONTACTS + leg] != 0.0) {        /* stance: tau = J' (-f_grf) (:303) */
+      for (int c = 0; c < 3; ++c) {
+        double s = 0.0;
+        for (int r = 0; r < 3; ++r) s += J[3 * r + c] * -f_grf[3 * leg + r];
+        t[c] = s;
+      }
+    } else {                                         /* swing: J tau = km .* f_kin (:306-307) */
+      double ft[3];
+      for (int r = 0; r < 3; ++r) ft[r] = tq[MPCQP_TQ_KM + r] * tq[MPCQP_TQ_FKIN + 3 * leg + r];
+      lu3_solve(J, ft, t);
+    }
+  }
+  for (int k = 0; k < 12; ++k) {
+    double v = jt[k] + tq[MPCQP_TQ_GRAV + k];        /* += torques_gravity (:311) */
+    if (!isnan(v)) tau[k] = v;                       /* NaN guard (:313-317) */
+  }
+}
+
+/* ============================================================================================
  * Batch over host threads (CPU baseline)
  * ========================================================================================== */
 

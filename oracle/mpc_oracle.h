@@ -70,6 +70,12 @@ int32_t orc_solver_step(orc_solver* s, const double* rec, mpcqp_result* res, dou
 int32_t orc_solve_sequence(const mpcqp_params* prm, const double* recs, int32_t T, int32_t batch,
                            mpcqp_result* res, int32_t nthreads);
 
+/* A1RobotControl::compute_joint_torques (A1RobotControl.cpp:289-319) for one robot: `tq` is an
+ * MPCQP_TQ_SIZE record (include/mpcqp.h), `f_grf` the 12 body-frame GRFs (foot_forces_grf
+ * columns, = mpcqp_result.f_body), `counter` the controller's mpc_init_counter (incremented),
+ * `tau` the robot's joint_torques (updated in place; NaN entries keep the previous value). */
+void orc_joint_torques(const double* tq, const double* f_grf, int32_t* counter, double* tau);
+
 /* Batch over `nthreads` POSIX threads (static contiguous partition).  sols may be NULL. */
 int32_t orc_solve_batch(const mpcqp_params* prm, const double* recs, int32_t batch,
                         mpcqp_result* res, double* sols, int32_t nthreads);

@@ -141,6 +141,8 @@ def lib():
         L.orc_solve_sequence.argtypes = [ctypes.POINTER(Params), dp, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_void_p, ctypes.c_int32]
         L.orc_solve_sequence.restype = ctypes.c_int32
+        L.orc_joint_torques.argtypes = [dp, dp, ctypes.POINTER(ctypes.c_int32), dp]
+        L.orc_joint_torques.restype = None
         _lib = L
     return _lib
 
@@ -240,3 +242,19 @@ def solve_sequence(params, recs, nthreads=1):
     rc = lib().orc_solve_sequence(ctypes.byref(params), _dp(recs), T, B, res.ctypes.data, nthreads)
     assert rc == 0
     return res
+
+
+TQ_SIZE = 68
+
+
+def joint_torques(tq_recs, f_grf, counters, tau):
+    """orc_joint_torques per robot: tq_recs [B,68], f_grf [B,12]; counters [B] int32 and
+    tau [B,12] are updated in place (compute_joint_torques, A1RobotControl.cpp:289-319)."""
+    tq_recs = np.ascontiguousarray(tq_recs, dtype=np.float64)
+    f_grf = np.ascontiguousarray(f_grf, dtype=np.float64)
+    assert counters.dtype == np.int32 and tau.dtype == np.float64 and tau.flags.c_contiguous
+    for b in range(tq_recs.shape[0]):
+        c = ctypes.c_int32(int(counters[b]))
+        row = tau[b]
+        lib().orc_joint_torques(_dp(tq_recs[b]), _dp(f_grf[b]), ctypes.byref(c), _dp(row))
+        counters[b] = c.value
