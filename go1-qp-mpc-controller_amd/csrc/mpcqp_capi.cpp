@@ -163,8 +163,9 @@ int32_t mpcqp_destroy(mpcqp_handle* h) {
 
 static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32_t batch,
                                  mpcqp_result* d_results, double* d_solution, double* d_trace,
-                                 int32_t trace_cap, void* stream) {
+                                 int32_t trace_cap, void* stream, double* d_state = nullptr) {
   if (!h || batch < 0 || (batch > 0 && (!d_records || !d_results))) return MPCQP_ERR_INVALID_ARG;
+  if (d_state && effective_path(h) != 3) return MPCQP_ERR_INVALID_ARG;  // warm start: wave path only
   if (batch == 0) return MPCQP_OK;
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
@@ -179,6 +180,7 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   a.work = h->work;
   a.trace = d_trace;
   a.trace_cap = d_trace ? trace_cap : 0;
+  a.wstate = d_state;
   a.grid = batch;
   a.stream = stream;
   a.p = h->p;
@@ -200,6 +202,17 @@ int32_t mpcqp_debug_solve_trace_device(mpcqp_handle* h, const double* d_records,
                                        mpcqp_result* d_results, double* d_solution,
                                        double* d_trace, int32_t trace_cap, void* stream) {
   return solve_device_impl(h, d_records, batch, d_results, d_solution, d_trace, trace_cap, stream);
+}
+
+int32_t mpcqp_warm_state_size(int32_t horizon) {
+  if (horizon < 1 || horizon > mpcqp::WAVE_MAX_HORIZON) return 0;
+  return mpcqp::warm_state_doubles(horizon);
+}
+
+int32_t mpcqp_solve_batch_warm_device(mpcqp_handle* h, const double* d_records, int32_t batch, double* d_state,
+                                      mpcqp_result* d_results, double* d_solution, void* stream) {
+  if (batch > 0 && !d_state) return MPCQP_ERR_INVALID_ARG;
+  return solve_device_impl(h, d_records, batch, d_results, d_solution, nullptr, 0, stream, d_state);
 }
 
 int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t batch,

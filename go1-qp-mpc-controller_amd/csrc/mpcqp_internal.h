@@ -17,6 +17,7 @@ struct LaunchArgs {
   double* work;
   double* trace;
   int trace_cap;
+  double* wstate;  // warm-start slots [batch][warm_state_doubles(N)] (wave path) or nullptr
   int grid;
   void* stream;
   mpcqp_params p;
@@ -40,6 +41,10 @@ hipError_t launch_wave_any(const LaunchArgs& a);
 hipError_t occupancy_wave_any(int horizon, int* blocks);
 hipError_t wave_selftest(double* d_out, void* stream);
 constexpr int WAVE_MAX_HORIZON = 20;
+// doubles per robot of the warm-start slot (mpcqp_wave.hip WarmLayout)
+__host__ __device__ constexpr int warm_state_doubles(int N) {
+  return 4 + 3 * 12 * N + 5 * 20 * N + ((12 * N + 63) / 64) * 12 * N;
+}
 
 // Downstream torque map (mpcqp_torque.hip)
 hipError_t launch_torques(const double* recs, const mpcqp_result* grf, int batch, int* counter, double* tau,

@@ -47,6 +47,18 @@ struct Cfg {
   static constexpr int REC = MPCQP_REC_SIZE(N);
 };
 
+// Warm-start slot of one robot (binary64, caller-owned device memory): everything the reference's
+// persistent OsqpEigen solver carries from one tick to the next.  Scaled quantities are stored as
+// the kernel used them; the zero pattern of H's upper triangle (one bit per entry, MW words per
+// column) decides between osqp_update_P and OsqpEigen's re-init on the next tick.
+template <int N>
+struct WarmLayout {
+  static constexpr int n = ND * N, m = CD * N, MW = (n + 63) / 64;
+  static constexpr int FLAG = 0, RHO = 1, C = 2, D = 4, E = D + n, QT = E + m, AK = QT + n, X = AK + 2 * m,
+                       Z = X + n, Y = Z + m, MASK = Y + m, SIZE = MASK + MW * n;
+  static_assert(SIZE == warm_state_doubles(N), "warm-start slot layout");
+};
+
 template <int N>
 struct WSmem {
   using C = Cfg<N>;
@@ -59,6 +71,8 @@ struct WSmem {
       double D[C::n], Dt[C::n], q[C::n], E[C::m];
       double lam[N][ND];  // gradient adjoint lambda_k (states 0..11)
       double vec[2][16];  // sequential 13-vectors (gradient forward sweep)
+      double Ap[2][C::m];  // unscaled A entries per row: [0] on fx / fy (rows 0-3), [1] on fz
+      double qn[C::n];     // this tick's gradient (warm start: q of the Ruiz passes is the old one)
     } h;
     struct Fs {  // solve: per-step factors + factorization scratch
       alignas(16) double Gi[N][144];
@@ -490,8 +504,9 @@ template <int N>
 __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ recs, int batch,
                                                      mpcqp_result* __restrict__ results,
                                                      double* __restrict__ solution, double* __restrict__ trace,
-                                                     int trace_cap, mpcqp_params p) {
+                                                     int trace_cap, double* __restrict__ wstate, mpcqp_params p) {
   using C = Cfg<N>;
+  using WL = WarmLayout<N>;
   constexpr int n = C::n, m = C::m, R = C::R;
   __shared__ WSmem<N> sm;
   const int inst = blockIdx.x;
@@ -606,13 +621,23 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   for (int j = t; j < n; j += NT) {
     const int k = j / ND, ii = j % ND;
     const double* lm = HS.lam[k];
-    HS.q[j] = ((sm.Bw[k][0][ii] * lm[6] + sm.Bw[k][1][ii] * lm[7]) + sm.Bw[k][2][ii] * lm[8]) + dtm * lm[9 + ii % 3];
+    const double g = ((sm.Bw[k][0][ii] * lm[6] + sm.Bw[k][1][ii] * lm[7]) + sm.Bw[k][2][ii] * lm[8]) + dtm * lm[9 + ii % 3];
+    HS.q[j] = g;
+    HS.qn[j] = g;
     HS.D[j] = 1.0;
   }
-  for (int r = t; r < m; r += NT) HS.E[r] = 1.0;
+  for (int r = t; r < m; r += NT) {
+    HS.E[r] = 1.0;
+    const int a5 = r % 5;  // friction pyramid rows (ConvexMpc.cpp:46-58)
+    HS.Ap[0][r] = a5 < 4 ? 1.0 : 0.0;
+    HS.Ap[1][r] = a5 < 4 ? ((a5 & 1) ? -mu : mu) : 1.0;
+  }
   wave_sync();
-  const double amu = dabs(mu);
-  auto colmax1 = [&](int c) __attribute__((always_inline)) -> double {  // max_i D_i |H_ic|
+  // Warm start (A1RobotControl.h:67 member solver, :522-538): the slot of the previous tick.
+  double* const ws = wstate ? wstate + (size_t)inst * WL::SIZE : nullptr;
+  const bool had = ws && ws[WL::FLAG] != 0.0;
+  auto colmax1 = [&](int c, unsigned long long (&zm)[WL::MW], auto with_mask) __attribute__((always_inline)) -> double {
+    // max_i D_i |H_ic|; zm collects the exact zeros of column c's upper triangle (sparseView)
     const int k = c / ND, a2 = c % ND;
     double y[12], w[12];
 #pragma unroll
@@ -680,36 +705,84 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         if (j == k && b == a2) hv += 2 * p.r_weights[b];
         if (b & 1) mx1 = fmax(mx1, dj[b] * dabs(hv));
         else mx0 = fmax(mx0, dj[b] * dabs(hv));
+        if constexpr (decltype(with_mask)::value) {
+          const int ri = ND * j + b;  // row index; its bit in word ri >> 6
+          const unsigned long long bit = (hv == 0.0 && ri <= c) ? (1ull << (ri & 63)) : 0ull;
+#pragma unroll
+          for (int w = 0; w < WL::MW; ++w) zm[w] |= (ri >> 6) == w ? bit : 0ull;
+        }
       }
     }
     return fmax(mx0, mx1);
   };
   constexpr int NC = (C::n + NT - 1) / NT;  // columns per lane: t, t + 64, ...
-  auto colmax = [&](double (&cm)[NC]) __attribute__((always_inline)) {
+  auto colmax = [&](double (&cm)[NC], bool masks) __attribute__((always_inline)) {
+    bool diff = false;
 #pragma unroll
-    for (int h = 0; h < NC; ++h) cm[h] = t + NT * h < n ? colmax1(t + NT * h) : 0.0;
+    for (int h = 0; h < NC; ++h) {
+      const int c = t + NT * h;
+      unsigned long long zm[WL::MW];
+#pragma unroll
+      for (int w = 0; w < WL::MW; ++w) zm[w] = 0ull;
+      if (masks) {
+        cm[h] = c < n ? colmax1(c, zm, IC<1>{}) : 0.0;
+      } else {
+        cm[h] = c < n ? colmax1(c, zm, IC<0>{}) : 0.0;
+      }
+      if (masks && c < n) {  // compare with and replace the previous tick's pattern
+        double* slot = ws + WL::MASK + WL::MW * c;
+#pragma unroll
+        for (int w = 0; w < WL::MW; ++w) {
+          diff |= __double_as_longlong(slot[w]) != (long long)zm[w];
+          slot[w] = __longlong_as_double((long long)zm[w]);
+        }
+      }
+    }
+    return __ballot(diff) != 0;
   };
-  // column norm of A~ for variable j / row norm of A~ for row r
+  // column norm of A~ for variable j / row norm of A~ for row r (A entries from HS.Ap)
   auto acol = [&](int j) __attribute__((always_inline)) {
     const int f = j / 3, aa = j % 3;
     const double* e = HS.E + 5 * f;
+    const double* a0 = HS.Ap[0] + 5 * f;
+    const double* a1 = HS.Ap[1] + 5 * f;
     double mx;
-    if (aa == 0) mx = dmax(e[0], e[1]);
-    else if (aa == 1) mx = dmax(e[2], e[3]);
-    else mx = dmax(dmax(dmax(dmax(amu * e[0], amu * e[1]), amu * e[2]), amu * e[3]), e[4]);
+    if (aa == 0) mx = dmax(e[0] * dabs(a0[0]), e[1] * dabs(a0[1]));
+    else if (aa == 1) mx = dmax(e[2] * dabs(a0[2]), e[3] * dabs(a0[3]));
+    else
+      mx = dmax(dmax(dmax(dmax(dabs(a1[0]) * e[0], dabs(a1[1]) * e[1]), dabs(a1[2]) * e[2]), dabs(a1[3]) * e[3]),
+                e[4] * dabs(a1[4]));
     return mx * HS.D[j];
   };
   auto arow = [&](int r) __attribute__((always_inline)) {
     const int f = r / 5, k5 = r % 5;
     const double e = HS.E[r];
     const double* d = HS.D + 3 * f;
-    if (k5 == 4) return e * d[2];
-    return dmax(e * d[k5 >> 1], (amu * e) * d[2]);
+    if (k5 == 4) return (e * dabs(HS.Ap[1][r])) * d[2];
+    return dmax((e * dabs(HS.Ap[0][r])) * d[k5 >> 1], (dabs(HS.Ap[1][r]) * e) * d[2]);
   };
   double c_s = 1.0, cm[NC];
 #pragma unroll
   for (int h = 0; h < NC; ++h) cm[h] = 0.0;
-  if (p.scaling > 0) colmax(cm);
+  // First column pass (D = 1): the raw norms, and H's zero pattern, which decides the warm-start
+  // branch of OsqpEigen 0.6.3 updateHessianMatrix: same pattern -> osqp_update_P (unscale with the
+  // old scaling, rescale with the previous A and q, keep iterates and rho); a changed pattern ->
+  // re-init (fresh scaling and rho) with the previous unscaled x, y restored (oracle ws_update).
+  const bool pattern_changed = (p.scaling > 0 || ws) ? colmax(cm, ws != nullptr) : false;
+  const int mode = !had ? 0 : (pattern_changed ? 2 : 1);  // 0 cold, 1 update_P, 2 re-init
+  if (mode == 1) {
+    // unscale_data with the previous scaling: q = D^-1 (c^-1 q~), A = (E^-1 A~) D^-1
+    const double cinv_o = 1. / ws[WL::C];
+    for (int j = t; j < n; j += NT) HS.q[j] = (1. / ws[WL::D + j]) * (cinv_o * ws[WL::QT + j]);
+    for (int r = t; r < m; r += NT) {
+      const int f = r / 5, k5 = r % 5;
+      const double ei = 1. / ws[WL::E + r];
+      const double d2 = 1. / ws[WL::D + 3 * f + 2];
+      HS.Ap[0][r] = k5 < 4 ? (ws[WL::AK + r] * ei) * (1. / ws[WL::D + 3 * f + (k5 >> 1)]) : 0.0;
+      HS.Ap[1][r] = (ws[WL::AK + m + r] * ei) * d2;
+    }
+    wave_sync();
+  }
   for (int pass = 0; pass < p.scaling; ++pass) {
 #pragma unroll
     for (int h = 0; h < NC; ++h) {
@@ -736,7 +809,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       HS.D[j] = HS.D[j] * HS.Dt[j];
     }
     wave_sync();
-    colmax(cm);  // column norms of the D-scaled P (cost normalization)
+    colmax(cm, false);  // column norms of the D-scaled P (cost normalization)
     double sv = 0.0, qv = 0.0;
 #pragma unroll
     for (int h = 0; h < NC; ++h) {
@@ -761,7 +834,8 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   WV_MARK(4);
 
   // ---- 4. lane registers: variables (D, q~) and rows (E, A~, bounds, rho) — set_rho_vec -----------
-  const double rho0 = dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
+  // update_P keeps the adapted rho (settings->rho); setup and re-init start from the settings'
+  const double rho0 = mode == 1 ? ws[WL::RHO] : dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
   double X[R], Qv[R], Dv[R], DI[R], PX[R], PXO[R], DX[R], RHS[R];
   double Z[R], Y[R], DY[R], Ev[R], AK0[R], AK1[R];
   double Z4[R], Y4[R], DY4[R], E4[R], L4[R], U4[R], AK4[R], RHO4[R];
@@ -777,13 +851,14 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     const int cf = ND * kc + 3 * leg;  // the leg's three variables
     Dv[r] = vv ? HS.D[ci] : 1.0;
     DI[r] = 1. / Dv[r];
-    Qv[r] = vv ? HS.q[ci] : 0.0;
+    // update_P then osqp_update_lin_cost: q~ = c (D q) of this tick's gradient
+    Qv[r] = vv ? (mode == 1 ? (HS.qn[ci] * Dv[r]) * c_s : HS.q[ci]) : 0.0;
     Ev[r] = kv ? HS.E[ri] : 1.0;
     E4[r] = kv ? HS.E[r4] : 1.0;
-    // A~ = E A D: row a < 4 has 1 on fx (a < 2) / fy (a >= 2) and +-mu on fz; row 4 has 1 on fz
-    AK0[r] = kv ? Ev[r] * HS.D[cf + (a >> 1)] : 0.0;
-    AK1[r] = kv ? (((a & 1) ? -mu : mu) * Ev[r]) * HS.D[cf + 2] : 0.0;
-    AK4[r] = kv ? E4[r] * HS.D[cf + 2] : 0.0;
+    // A~ = E A D: row a < 4 has A on fx (a < 2) / fy (a >= 2) and on fz; row 4 on fz
+    AK0[r] = kv ? (HS.Ap[0][ri] * Ev[r]) * HS.D[cf + (a >> 1)] : 0.0;
+    AK1[r] = kv ? (HS.Ap[1][ri] * Ev[r]) * HS.D[cf + 2] : 0.0;
+    AK4[r] = kv ? (HS.Ap[1][r4] * E4[r]) * HS.D[cf + 2] : 0.0;
     // bounds (ConvexMpc.cpp:223-245), clipped to +-OSQP_INFTY, scaled by E
     double l4 = fzmin * cont, u4 = fzmax * cont;
     l4 = dmin(dmax(l4, -OSQP_INF), OSQP_INF);
@@ -793,6 +868,26 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     X[r] = 0.0; PX[r] = 0.0; PXO[r] = 0.0; DX[r] = 0.0;
     Z[r] = 0.0; Y[r] = 0.0; DY[r] = 0.0; Z4[r] = 0.0; Y4[r] = 0.0; DY4[r] = 0.0;
     RHS[r] = vv ? sigma * 0.0 - Qv[r] : 0.0;  // cold start: compute_rhs with x = z = y = 0
+    if (mode == 1) {  // warm start: the previous scaled iterates as they are
+      X[r] = vv ? ws[WL::X + ci] : 0.0;
+      Z[r] = kv ? ws[WL::Z + ri] : 0.0;
+      Y[r] = kv ? ws[WL::Y + ri] : 0.0;
+      Z4[r] = kv ? ws[WL::Z + r4] : 0.0;
+      Y4[r] = kv ? ws[WL::Y + r4] : 0.0;
+    } else if (mode == 2) {  // re-init: x = D^-1 (D_old x_old), y = c E^-1 ((E_old y_old) c_old^-1)
+      const double cinv_o = 1. / ws[WL::C];
+      X[r] = vv ? DI[r] * (ws[WL::D + ci] * ws[WL::X + ci]) : 0.0;
+      Y[r] = kv ? c_s * ((1. / Ev[r]) * ((ws[WL::E + ri] * ws[WL::Y + ri]) * cinv_o)) : 0.0;
+      Y4[r] = kv ? c_s * ((1. / E4[r]) * ((ws[WL::E + r4] * ws[WL::Y + r4]) * cinv_o)) : 0.0;
+    }
+  }
+  if (mode == 2) {  // z = A~ x
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double xp = dpp<QP_PRIM>(X[r]), xz = dpp<QP_B2>(X[r]);
+      Z[r] = AK0[r] * xp + AK1[r] * xz;
+      Z4[r] = AK4[r] * xz;
+    }
   }
   auto rho4_of = [&](int r, double rho) __attribute__((always_inline)) {
     const bool loose = L4[r] < -OSQP_INF * MIN_SCALING && U4[r] > OSQP_INF * MIN_SCALING;
@@ -801,6 +896,54 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   };
 #pragma unroll
   for (int r = 0; r < R; ++r) RHO4[r] = rho4_of(r, rho0);
+  if (mode != 0) {
+    // P~x of the warm iterate (the loop carries P~x through the KKT identity from here):
+    // P~x = c D H (D x), H v = B_qp' Q B_qp v + R v by the dynamics: x_{i+1} = A x_i + B_i v_i
+    // from x_0 = 0, e_i = Q x_{i+1}, lambda_j = e_j + A' lambda_{j+1}, (H v)_j = B_j' lambda_j + R v_j.
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (vvr[r]) HS.Dt[ND * (4 * r + ig) + idx] = Dv[r] * X[r];
+    if (t < 16) HS.vec[0][t] = 0.0;
+    wave_sync();
+    for (int i = 0; i < N; ++i) {
+      if (t < ND) {
+        const double* pv = HS.vec[i & 1];
+        const double* v = HS.Dt + ND * i;
+        double s;
+        if (t == 0) s = (pv[0] + A.ad0 * pv[6]) + A.ad1 * pv[7];
+        else if (t == 1) s = (pv[1] + (-A.ad1) * pv[6]) + A.ad0 * pv[7];
+        else if (t == 2) s = pv[2] + dt * pv[8];
+        else if (t <= 5) s = pv[t] + dt * pv[t + 6];
+        else s = pv[t];
+        double bu = 0.0;
+        if (t >= 6 && t < 9) {
+          const double* bw = sm.Bw[i][t - 6];
+          for (int c2 = 0; c2 < ND; ++c2) bu += bw[c2] * v[c2];
+        } else if (t >= 9) {
+          bu = dtm * (((v[t - 9] + v[t - 6]) + v[t - 3]) + v[t]);
+        }
+        const double xn = s + bu;
+        HS.vec[(i + 1) & 1][t] = xn;
+        HS.lam[i][t] = 2 * p.q_weights[t] * xn;
+      }
+      wave_sync();
+    }
+    for (int j = N - 2; j >= 0; --j) {
+      if (t < ND) HS.lam[j][t] = HS.lam[j][t] + A.atv(t, HS.lam[j + 1]);
+      wave_sync();
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int k = vvr[r] ? 4 * r + ig : 0;
+      const double* lm = HS.lam[k];
+      const double hv = (((sm.Bw[k][0][idx] * lm[6] + sm.Bw[k][1][idx] * lm[7]) + sm.Bw[k][2][idx] * lm[8]) +
+                         dtm * lm[9 + idx % 3]) + (2 * p.r_weights[idx]) * HS.Dt[ND * k + idx];
+      PX[r] = vvr[r] ? (c_s * Dv[r]) * hv : 0.0;
+      // compute_rhs from the warm x, z, y: sigma x - q~ + A~'(rho z - y)
+      const double at = quad_at(rho0 * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
+      RHS[r] = vvr[r] ? (sigma * X[r] - Qv[r]) + at : 0.0;
+    }
+  }
   // rows 0-3: l = 0 / u = +inf (rows 0, 2) or l = -inf / u = 0 (rows 1, 3): always inequalities
   auto lo03 = [&](int r) __attribute__((always_inline)) { return (a & 1) ? Ev[r] * -OSQP_INF : Ev[r] * 0.0; };
   auto hi03 = [&](int r) __attribute__((always_inline)) { return (a & 1) ? Ev[r] * 0.0 : Ev[r] * OSQP_INF; };
@@ -1168,6 +1311,38 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   }
 
   WV_MARK(20);
+  if (ws) {  // the solver persists: scaling, scaled data, iterates and rho for the next tick
+    if (t == 0) {
+      ws[WL::FLAG] = 1.0;
+      ws[WL::RHO] = rho;
+      ws[WL::C] = cost_c;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int k = 4 * r + ig;
+      if (vvr[r]) {
+        const int ci = ND * k + idx;
+        ws[WL::D + ci] = Dv[r];
+        ws[WL::QT + ci] = Qv[r];
+        ws[WL::X + ci] = X[r];
+      }
+      if (kvr[r]) {
+        const int ri = CD * k + 5 * leg + a, r4 = CD * k + 5 * leg + 4;
+        ws[WL::E + ri] = Ev[r];
+        ws[WL::AK + ri] = AK0[r];
+        ws[WL::AK + m + ri] = AK1[r];
+        ws[WL::Z + ri] = Z[r];
+        ws[WL::Y + ri] = Y[r];
+        if (a == 0) {
+          ws[WL::E + r4] = E4[r];
+          ws[WL::AK + r4] = 0.0;
+          ws[WL::AK + m + r4] = AK4[r];
+          ws[WL::Z + r4] = Z4[r];
+          ws[WL::Y + r4] = Y4[r];
+        }
+      }
+    }
+  }
   // ---- 6. store_solution + unscale + compute_grf extraction (A1RobotControl.cpp:555-561) --------
   const bool has_sol = status != MPCQP_STATUS_PRIMAL_INFEASIBLE &&
                        status != MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE &&
@@ -1237,7 +1412,7 @@ __global__ void wave_selftest_kernel(double* out) {
 template <int N>
 static hipError_t launch_wave(const LaunchArgs& a) {
   hipLaunchKernelGGL((wv::wave_kernel<N>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs, a.batch,
-                     a.results, a.solution, a.trace, a.trace_cap, a.p);
+                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.p);
   return hipGetLastError();
 }
 template <int N>

@@ -90,6 +90,7 @@ EXPORTED = [
     "mpcqp_status_str", "mpcqp_error_str", "mpcqp_last_error",
     "mpcqp_debug_solve_trace_device", "mpcqp_abi_sizes", "mpcqp_handle_slots", "mpcqp_solve_threads",
     "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_joint_torques_device",
+    "mpcqp_warm_state_size", "mpcqp_solve_batch_warm_device",
 ]
 
 _lib = None
@@ -144,6 +145,10 @@ def load():
     L.mpcqp_debug_wave_selftest.restype = i32
     L.mpcqp_joint_torques_device.argtypes = [vp, vp, i32, vp, vp, vp]
     L.mpcqp_joint_torques_device.restype = i32
+    L.mpcqp_warm_state_size.argtypes = [i32]
+    L.mpcqp_warm_state_size.restype = i32
+    L.mpcqp_solve_batch_warm_device.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+    L.mpcqp_solve_batch_warm_device.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):

@@ -62,6 +62,18 @@ class MpcQpSolver:
                                                d_solution or None, stream or None),
               self._h, "mpcqp_solve_batch_device")
 
+    @property
+    def warm_state_size(self):
+        """Doubles per robot of the warm-start slot (mpcqp_warm_state_size)."""
+        return self._L.mpcqp_warm_state_size(self.horizon)
+
+    def solve_warm_device(self, d_records, batch, d_state, d_results, d_solution=0, stream=0):
+        """mpcqp_solve_batch_warm_device: the reference's persistent, warm-started solver per robot
+        (A1RobotControl.cpp:522-540); d_state [batch][warm_state_size] doubles, zeroed at first."""
+        check(self._L.mpcqp_solve_batch_warm_device(self._h, d_records, int(batch), d_state, d_results,
+                                                    d_solution or None, stream or None),
+              self._h, "mpcqp_solve_batch_warm_device")
+
     def solve_device_trace(self, d_records, batch, d_results, d_solution, d_trace, trace_cap, stream=0):
         check(self._L.mpcqp_debug_solve_trace_device(self._h, d_records, int(batch), d_results,
                                                      d_solution or None, d_trace, int(trace_cap),

@@ -144,6 +144,18 @@ int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch);
 int32_t mpcqp_solve_batch_device(mpcqp_handle* h, const double* d_records, int32_t batch,
                                  mpcqp_result* d_results, double* d_solution, void* stream);
 
+/* Warm start across control ticks: the reference keeps one OsqpEigen::Solver per controller
+ * (A1RobotControl.h:67) with setWarmStart(true) (A1RobotControl.cpp:524); its first tick runs
+ * initSolver, later ticks updateHessianMatrix / updateGradient / updateLowerBound /
+ * updateUpperBound and solve from the previous x, z, y and adapted rho (:522-540).  The engine
+ * keeps that solver state per robot in a caller-owned DEVICE buffer
+ *   d_state [batch][mpcqp_warm_state_size(N)] binary64, zero-filled = "not initialized yet",
+ * so a robot's slot must follow it from tick to tick (same batch index).  Robots whose record
+ * is non-finite leave their slot untouched.  Default (wave) solver path only. */
+int32_t mpcqp_warm_state_size(int32_t horizon);
+int32_t mpcqp_solve_batch_warm_device(mpcqp_handle* h, const double* d_records, int32_t batch, double* d_state,
+                                      mpcqp_result* d_results, double* d_solution, void* stream);
+
 /* Host-pointer convenience wrapper (copies in, solves, copies out, synchronizes). */
 int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t batch,
                                mpcqp_result* h_results, double* h_solution);

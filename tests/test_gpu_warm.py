@@ -1,0 +1,102 @@
+"""Warm start across control ticks on the device vs the oracle's persistent
+solver (oracle/mpc_oracle.c orc_solver_step: OsqpEigen 0.6.3 initSolver on the first tick, then
+updateHessianMatrix / updateGradient / updateLowerBound / updateUpperBound and a warm-started
+solve; A1RobotControl.cpp:522-540).  Gates per tick: SURVEY §8(c) P1 (u0 within 1e-4 relative,
+status identical, iterations within one check interval)."""
+import numpy as np
+import pytest
+import torch
+
+import mpcqp
+from gpu_helpers import rel_err_u0, solve_gpu
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_sequence(oracle, params, recs_t):
+    op = oracle.default_params(params.horizon, q=list(params.q_weights), r=list(params.r_weights))
+    T, B = recs_t.shape[:2]
+    return oracle.solve_sequence(op, recs_t, nthreads=8)
+
+
+def _gpu_sequence(params, recs_t):
+    T, B = recs_t.shape[:2]
+    out = np.zeros((T, B), dtype=mpcqp.RESULT_DTYPE)
+    with mpcqp.MpcQpSolver(params) as s:
+        d_state = torch.zeros((B, s.warm_state_size), dtype=torch.float64, device="cuda")
+        d_res = torch.zeros((B, mpcqp._lib.RESULT_DOUBLES), dtype=torch.float64, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        for t in range(T):
+            d_rec = torch.from_numpy(np.ascontiguousarray(recs_t[t])).cuda()
+            s.solve_warm_device(d_rec.data_ptr(), B, d_state.data_ptr(), d_res.data_ptr(), 0, stream)
+            torch.cuda.synchronize()
+            out[t] = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
+    return out
+
+
+def _check(got, ref, label, min_iter_equal=0.9):
+    for t in range(got.shape[0]):
+        np.testing.assert_array_equal(got[t]["status"], ref[t]["status"], err_msg=f"{label} tick {t}")
+        ok = ref[t]["status"] != mpcqp._lib.STATUS_NAN_INPUT  # those carry NaN forces on both sides
+        err = rel_err_u0(got[t]["u0"][ok], ref[t]["u0"][ok])
+        assert np.all(err <= 1e-4), f"{label} tick {t}: worst {err.max():.3g}"
+        di = np.abs(got[t]["iters"].astype(int) - ref[t]["iters"].astype(int))
+        assert di.max() <= 25, f"{label} tick {t}: iteration drift {di.max()}"
+        assert np.mean(di == 0) >= min_iter_equal, f"{label} tick {t}: {np.mean(di == 0):.2f} equal"
+
+
+@pytest.mark.parametrize("gait", ["trot", "stance"])
+def test_warm_sequence_matches_oracle(oracle, gait):
+    T, B, N = 12, 96, 10
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=31, gait=gait, swing_ticks=5)
+    recs_t = np.stack([mpcqp.assemble_compute_grf(s, N) for s in ticks])
+    p = mpcqp.default_params(N)
+    got = _gpu_sequence(p, recs_t)
+    ref = _oracle_sequence(oracle, p, recs_t)
+    _check(got, ref, f"warm {gait}")
+    # the first tick is a cold solve, bit for bit the cold kernel's
+    with mpcqp.MpcQpSolver(p) as s:
+        cold, _, _ = solve_gpu(s, recs_t[0])
+    np.testing.assert_array_equal(got[0]["u0"], cold["u0"])
+    np.testing.assert_array_equal(got[0]["iters"], cold["iters"])
+    # warm starting pays: fewer iterations than cold solves of the same ticks
+    cold_iters = np.stack([oracle.solve_batch(oracle.default_params(N), recs_t[t], nthreads=8)["iters"]
+                           for t in range(1, T)])
+    assert got[1:]["iters"].mean() < cold_iters.mean()
+
+
+def test_warm_pattern_change_reinit(oracle):
+    """test_mpc's stance has exact zeros in H (upper triangle); a rotated copy is dense.  Going
+    sparse -> dense -> dense -> sparse takes OsqpEigen's re-init branch, update_P, re-init."""
+    rec, q, r = mpcqp.assemble_test_mpc(10)
+    p = mpcqp.default_params(10, q_weights=q, r_weights=r)
+    P0, *_ = oracle.build_qp(oracle.default_params(10, q=list(q), r=list(r)), rec)
+    assert np.sum(np.triu(P0) == 0) > 120 * 119 // 2  # exact zeros above the diagonal
+    def rotated(yaw):
+        x = rec.copy()
+        c, s_ = np.cos(yaw), np.sin(yaw)
+        Rz = np.array([[c, -s_, 0], [s_, c, 0], [0, 0, 1.0]])
+        x[mpcqp._lib.REC_EULER + 2] = yaw
+        x[mpcqp._lib.REC_X0 + 2] = yaw
+        x[mpcqp._lib.REC_ROT:mpcqp._lib.REC_ROT + 9] = Rz.reshape(9)
+        f = mpcqp._lib.rec_feet(10)
+        feet = x[f:f + 120].reshape(10, 4, 3)
+        x[f:f + 120] = np.einsum("ij,klj->kli", Rz, feet).reshape(120)
+        return x
+    seq = np.stack([rec, rotated(0.3), rotated(0.31), rec])[:, None, :]
+    got = _gpu_sequence(p, seq)
+    ref = _oracle_sequence(oracle, p, seq)
+    _check(got, ref, "pattern change", min_iter_equal=1.0)
+
+
+def test_warm_nan_tick_leaves_state(oracle):
+    T, B = 4, 8
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=5, gait="stance")
+    recs_t = np.stack([mpcqp.assemble_compute_grf(s, 10) for s in ticks])
+    bad = recs_t.copy()
+    bad[2, 3, 7] = np.nan
+    p = mpcqp.default_params(10)
+    got = _gpu_sequence(p, bad)
+    assert got[2]["status"][3] == mpcqp._lib.STATUS_NAN_INPUT
+    ref = _oracle_sequence(oracle, p, bad)
+    _check(got, ref, "nan tick")
