@@ -264,6 +264,27 @@ int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t 
   return MPCQP_OK;
 }
 
+void mpcqp_balance_default_params(mpcqp_balance_params* p) {
+  if (!p) return;
+  const double q[6] = {1.0, 1.0, 1.0, 400.0, 400.0, 100.0};  // A1RobotControl.cpp:11
+  for (int i = 0; i < 6; ++i) p->q_diag[i] = q[i];
+  p->r = 1e-3;  // :12
+  p->mu = 0.7;  // :13
+  p->f_min = 0.0;
+  p->f_max = 180.0;  // :14-15
+}
+
+int32_t mpcqp_balance_solve_device(mpcqp_handle* h, const mpcqp_balance_params* bp, const double* d_records,
+                                   int32_t batch, mpcqp_result* d_results, void* stream) {
+  if (!h || !bp || batch < 0 || (batch > 0 && (!d_records || !d_results))) return MPCQP_ERR_INVALID_ARG;
+  if (batch == 0) return MPCQP_OK;
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
+  e = mpcqp::launch_balance(*bp, h->p, d_records, batch, d_results, stream);
+  if (e != hipSuccess) return set_hip_error(h, e, "balance_kernel launch");
+  return MPCQP_OK;
+}
+
 int32_t mpcqp_joint_torques_device(const double* d_tq_records, const mpcqp_result* d_grf, int32_t batch,
                                    int32_t* d_counter, double* d_joint_torques, void* stream) {
   if (batch < 0 || (batch > 0 && (!d_tq_records || !d_grf || !d_counter || !d_joint_torques)))

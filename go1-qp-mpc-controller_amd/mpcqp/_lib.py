@@ -66,6 +66,12 @@ class Params(ctypes.Structure):
     ]
 
 
+class BalanceParams(ctypes.Structure):
+    """mpcqp_balance_params."""
+    _fields_ = [("q_diag", ctypes.c_double * 6), ("r", ctypes.c_double), ("mu", ctypes.c_double),
+                ("f_min", ctypes.c_double), ("f_max", ctypes.c_double)]
+
+
 class Result(ctypes.Structure):
     """mpcqp_result."""
     _fields_ = [
@@ -91,6 +97,7 @@ EXPORTED = [
     "mpcqp_debug_solve_trace_device", "mpcqp_abi_sizes", "mpcqp_handle_slots", "mpcqp_solve_threads",
     "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_joint_torques_device",
     "mpcqp_warm_state_size", "mpcqp_solve_batch_warm_device",
+    "mpcqp_balance_default_params", "mpcqp_balance_solve_device",
 ]
 
 _lib = None
@@ -149,6 +156,10 @@ def load():
     L.mpcqp_warm_state_size.restype = i32
     L.mpcqp_solve_batch_warm_device.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     L.mpcqp_solve_batch_warm_device.restype = i32
+    L.mpcqp_balance_default_params.argtypes = [ctypes.POINTER(BalanceParams)]
+    L.mpcqp_balance_default_params.restype = None
+    L.mpcqp_balance_solve_device.argtypes = [vp, ctypes.POINTER(BalanceParams), vp, i32, vp, vp]
+    L.mpcqp_balance_solve_device.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):
@@ -170,6 +181,19 @@ def default_params(horizon=10, **over):
         else:
             setattr(p, k, v)
     return p
+
+
+def default_balance_params(**over):
+    """mpcqp_balance_default_params (A1RobotControl.cpp:11-15) + keyword overrides."""
+    bp = BalanceParams()
+    load().mpcqp_balance_default_params(ctypes.byref(bp))
+    for k, v in over.items():
+        if k == "q_diag":
+            for i, x in enumerate(v):
+                bp.q_diag[i] = float(x)
+        else:
+            setattr(bp, k, v)
+    return bp
 
 
 def check(rc, handle=None, what="mpcqp"):

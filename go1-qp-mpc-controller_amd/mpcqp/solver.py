@@ -62,6 +62,11 @@ class MpcQpSolver:
                                                d_solution or None, stream or None),
               self._h, "mpcqp_solve_batch_device")
 
+    def balance_solve_device(self, bp, d_records, batch, d_results, stream=0):
+        """Single-step QP balance controller (mpcqp_balance_solve_device): records [batch][72]."""
+        check(self._L.mpcqp_balance_solve_device(self._h, ctypes.byref(bp), d_records, int(batch),
+                                                 d_results, stream or None), self._h, "mpcqp_balance_solve_device")
+
     @property
     def warm_state_size(self):
         """Doubles per robot of the warm-start slot (mpcqp_warm_state_size)."""

@@ -183,6 +183,48 @@ int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t 
 int32_t mpcqp_joint_torques_device(const double* d_tq_records, const mpcqp_result* d_grf, int32_t batch,
                                    int32_t* d_counter, double* d_joint_torques, void* stream);
 
+/* ---- single-step QP balance controller: the stance_leg_control_type == 0 branch of
+ * A1RobotControl::compute_grf (A1RobotControl.cpp:321-332 euler error, :377-444 QP), constants
+ * from the A1RobotControl ctor (:7-48).  12 variables (world-frame GRF), 20 rows (4 fz bounds,
+ * 16 friction-pyramid rows), a fresh OsqpEigen::Solver every tick (warm start off, :420).
+ * One binary64 record per robot (offsets in doubles; matrices row-major).                    */
+#define MPCQP_BAL_POS 0        /* [3] root_pos (world)                                       */
+#define MPCQP_BAL_POS_D 3      /* [3] root_pos_d                                             */
+#define MPCQP_BAL_ROT 6        /* [9] root_rot_mat                                           */
+#define MPCQP_BAL_ROT_Z 15     /* [9] root_rot_mat_z (yaw-only rotation)                     */
+#define MPCQP_BAL_LIN_VEL 24   /* [3] root_lin_vel (world)                                   */
+#define MPCQP_BAL_LIN_VEL_D 27 /* [3] root_lin_vel_d (body, as :382 reads it)                */
+#define MPCQP_BAL_ANG_VEL 30   /* [3] root_ang_vel (world)                                   */
+#define MPCQP_BAL_ANG_VEL_D 33 /* [3] root_ang_vel_d (body)                                  */
+#define MPCQP_BAL_EULER 36     /* [3] root_euler                                             */
+#define MPCQP_BAL_EULER_D 39   /* [3] root_euler_d                                           */
+#define MPCQP_BAL_KP_LIN 42    /* [3] kp_linear                                              */
+#define MPCQP_BAL_KD_LIN 45    /* [3] kd_linear                                              */
+#define MPCQP_BAL_KP_ANG 48    /* [3] kp_angular                                             */
+#define MPCQP_BAL_KD_ANG 51    /* [3] kd_angular                                             */
+#define MPCQP_BAL_MASS 54      /* robot_mass                                                 */
+#define MPCQP_BAL_FEET 55      /* [4][3] foot_pos_abs column i (world-aligned, body origin)   */
+#define MPCQP_BAL_CONTACTS 67  /* [4] contacts[i] as 0.0 / 1.0                               */
+#define MPCQP_BAL_SIZE 72      /* 71 used, padded to a multiple of 4 doubles                 */
+
+typedef struct mpcqp_balance_params {
+  double q_diag[6]; /* Q.diagonal() = 1, 1, 1, 400, 400, 100 (A1RobotControl.cpp:11)   */
+  double r;         /* R = 1e-3 (:12)                                                    */
+  double mu;        /* 0.7 (:13)                                                         */
+  double f_min;     /* F_min = 0 (:14)                                                   */
+  double f_max;     /* F_max = 180 (:15)                                                 */
+} mpcqp_balance_params;
+
+void mpcqp_balance_default_params(mpcqp_balance_params* p);
+
+/* Replaces the QP branch of compute_grf for `batch` robots (DEVICE pointers, async on `stream`):
+ * root_acc, H = R I + M'QM, g = -M'Q root_acc, bounds from contacts, OSQP setup + solve with the
+ * handle's OSQP settings (warm_start ignored: the reference builds a new solver each tick).
+ * d_results[b].u0 = QPSolution (world), .f_body = root_rot_mat^T QPSolution per leg (no NaN
+ * guard in this branch, :440-443: a NaN solution stays NaN and sets nan_legs). */
+int32_t mpcqp_balance_solve_device(mpcqp_handle* h, const mpcqp_balance_params* bp, const double* d_records,
+                                   int32_t batch, mpcqp_result* d_results, void* stream);
+
 const char* mpcqp_status_str(int32_t status);
 const char* mpcqp_error_str(int32_t err);
 /* Last HIP error string recorded by the handle (for MPCQP_ERR_HIP). */

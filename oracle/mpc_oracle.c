@@ -1010,11 +1010,18 @@ static void ws_free(osqp_ws* w) {
 
 /* osqp_setup on the QP of `rec` (OsqpEigen::Solver::initSolver, A1RobotControl.cpp:521-531):
  * data copy, bound clipping, scale_data, set_rho_vec, KKT factorization; x = z = y = 0. */
+static int ws_setup_dense(osqp_ws* w, double* Pd, double* Ad);
 static int ws_setup(osqp_ws* w, const double* rec) {
   const int n = w->n, m = w->m;
   double* Pd = (double*)malloc(sizeof(double) * (size_t)n * n);
   double* Ad = (double*)malloc(sizeof(double) * (size_t)m * n);
   orc_build_qp(w->st, rec, Pd, w->q, w->l, w->u, Ad);
+  return ws_setup_dense(w, Pd, Ad);
+}
+/* osqp_setup from dense P (full symmetric) and A (row-major) with q, l, u already in `w`;
+ * frees Pd and Ad. */
+static int ws_setup_dense(osqp_ws* w, double* Pd, double* Ad) {
+  const int n = w->n, m = w->m;
   /* OsqpEigen::Data::setHessianMatrix keeps triangularView<Upper> of hessian.sparseView() */
   csc_free(&w->P);
   csc_free(&w->A);
@@ -1425,6 +1432,127 @@ void orc_joint_torques(const double* tq, const double* f_grf, int32_t* counter, 
 }
 
 /* ============================================================================================
+ * Single-step QP balance controller (stance_leg_control_type == 0)
+ * ========================================================================================== */
+
+/* A1RobotControl.cpp:321-332 (euler error, yaw wrapped at 1.5 pi with the literal 3.1415926),
+ * :379-392 (root_acc), :394-407 (inertia_inv, H, g), ctor :27-44 (constraint rows), :410-414
+ * (fz bounds from contacts).  OsqpEigen::INFTY lower bounds on the 16 friction rows (:31-43),
+ * upper bounds 0 (setZero, :21). */
+void orc_balance_build_qp(const mpcqp_balance_params* bp, const double* rec, double* P, double* q,
+                          double* l, double* u, double* A) {
+  const double* R = rec + MPCQP_BAL_ROT;
+  const double* Rz = rec + MPCQP_BAL_ROT_Z;
+  double ee[3];
+  for (int k = 0; k < 3; ++k) ee[k] = rec[MPCQP_BAL_EULER_D + k] - rec[MPCQP_BAL_EULER + k];
+  if (ee[2] > 3.1415926 * 1.5)
+    ee[2] = rec[MPCQP_BAL_EULER_D + 2] - 3.1415926 * 2 - rec[MPCQP_BAL_EULER + 2];
+  else if (ee[2] < -3.1415926 * 1.5)
+    ee[2] = rec[MPCQP_BAL_EULER_D + 2] + 3.1415926 * 2 - rec[MPCQP_BAL_EULER + 2];
+  double acc[6], tv[3], tw[3];
+  for (int i = 0; i < 3; ++i) { /* R^T v */
+    double sv = 0.0, sw = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      sv += R[k * 3 + i] * rec[MPCQP_BAL_LIN_VEL + k];
+      sw += R[k * 3 + i] * rec[MPCQP_BAL_ANG_VEL + k];
+    }
+    tv[i] = rec[MPCQP_BAL_KD_LIN + i] * (rec[MPCQP_BAL_LIN_VEL_D + i] - sv);
+    tw[i] = sw;
+  }
+  for (int i = 0; i < 3; ++i) {
+    double s = 0.0;
+    for (int k = 0; k < 3; ++k) s += R[i * 3 + k] * tv[k];
+    acc[i] = rec[MPCQP_BAL_KP_LIN + i] * (rec[MPCQP_BAL_POS_D + i] - rec[MPCQP_BAL_POS + i]) + s;
+    acc[3 + i] = rec[MPCQP_BAL_KP_ANG + i] * ee[i] +
+                 rec[MPCQP_BAL_KD_ANG + i] * (rec[MPCQP_BAL_ANG_VEL_D + i] - tw[i]);
+  }
+  acc[2] += rec[MPCQP_BAL_MASS] * 9.8;
+  /* inertia_inv M (6 x 12): [I_3; Rz^T skew(foot_i)] per leg */
+  double M[6][12];
+  for (int leg = 0; leg < NL; ++leg) {
+    const double* f = rec + MPCQP_BAL_FEET + 3 * leg;
+    const double S[9] = {0.0, -f[2], f[1], f[2], 0.0, -f[0], -f[1], f[0], 0.0}; /* Utils.cpp:35-41 */
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        M[a][3 * leg + b] = a == b ? 1.0 : 0.0;
+        double s = 0.0;
+        for (int k = 0; k < 3; ++k) s += Rz[k * 3 + a] * S[k * 3 + b];
+        M[3 + a][3 * leg + b] = s;
+      }
+  }
+  for (int i = 0; i < ND; ++i) {
+    for (int j = 0; j < ND; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < 6; ++k) s += (M[k][i] * bp->q_diag[k]) * M[k][j];
+      P[i * ND + j] = (i == j ? bp->r : 0.0) + s;
+    }
+    double g = 0.0;
+    for (int k = 0; k < 6; ++k) g += (-M[k][i] * bp->q_diag[k]) * acc[k];
+    q[i] = g;
+  }
+  memset(A, 0, sizeof(double) * CD * ND);
+  for (int leg = 0; leg < NL; ++leg) {
+    const double c = rec[MPCQP_BAL_CONTACTS + leg] != 0.0 ? 1.0 : 0.0;
+    A[leg * ND + 3 * leg + 2] = 1.0;
+    l[leg] = c * bp->f_min;
+    u[leg] = c * bp->f_max;
+    for (int r = 0; r < 4; ++r) {
+      const int row = NL + 4 * leg + r;
+      A[row * ND + 3 * leg + (r >> 1)] = (r & 1) ? -1.0 : 1.0;
+      A[row * ND + 3 * leg + 2] = -bp->mu;
+      l[row] = -OSQP_INFTY;
+      u[row] = 0.0;
+    }
+  }
+}
+
+int32_t orc_balance_solve(const mpcqp_params* prm, const mpcqp_balance_params* bp, const double* rec,
+                          mpcqp_result* res) {
+  if (!prm || !bp || !rec || !res) return MPCQP_ERR_INVALID_ARG;
+  memset(res, 0, sizeof(*res));
+  for (int k = 0; k < MPCQP_BAL_SIZE - 1; ++k)
+    if (!isfinite(rec[k])) {
+      res->status = MPCQP_STATUS_NAN_INPUT;
+      res->nan_legs = 0xF;
+      for (int i = 0; i < ND; ++i) res->u0[i] = res->f_body[i] = OSQP_NAN;
+      return MPCQP_OK;
+    }
+  mpcqp_params p1 = *prm; /* a new OsqpEigen::Solver per tick, warm start off (:416-421) */
+  p1.horizon = 1;
+  p1.warm_start = 0;
+  osqp_ws w;
+  ws_alloc(&w, &p1);
+  double* Pd = (double*)malloc(sizeof(double) * ND * ND);
+  double* Ad = (double*)malloc(sizeof(double) * CD * ND);
+  orc_balance_build_qp(bp, rec, Pd, w.q, w.l, w.u, Ad);
+  int fail = ws_setup_dense(&w, Pd, Ad);
+  ws_admm(&w, fail, NULL, 0, NULL);
+  /* getSolution (NaN unless a solution exists) and foot_forces_grf = R^T x per leg (:440-443) */
+  const double* R = rec + MPCQP_BAL_ROT;
+  double xs[ND];
+  for (int i = 0; i < ND; ++i) xs[i] = has_solution(w.status) ? w.D[i] * w.x[i] : OSQP_NAN;
+  for (int leg = 0; leg < NL; ++leg) {
+    const double* f = xs + 3 * leg;
+    if (isnan(f[0] + f[1] + f[2])) res->nan_legs |= 1 << leg;
+    for (int r = 0; r < 3; ++r) {
+      double s = 0.0;
+      for (int c = 0; c < 3; ++c) s += R[c * 3 + r] * f[c];
+      res->f_body[3 * leg + r] = s;
+    }
+  }
+  memcpy(res->u0, xs, sizeof(xs));
+  res->obj_val = w.obj_val;
+  res->pri_res = w.pri_res;
+  res->dua_res = w.dua_res;
+  res->rho = w.rho;
+  res->status = w.status;
+  res->iters = w.iter;
+  res->rho_updates = w.rho_updates;
+  ws_free(&w);
+  return MPCQP_OK;
+}
+
+/* ============================================================================================
  * Batch over host threads (CPU baseline)
  * ========================================================================================== */
 
@@ -1465,5 +1593,41 @@ int32_t orc_solve_batch(const mpcqp_params* prm, const double* recs, int32_t bat
   for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   free(th);
   free(args);
+  return MPCQP_OK;
+}
+
+typedef struct {
+  const mpcqp_params* prm;
+  const mpcqp_balance_params* bp;
+  const double* recs;
+  mpcqp_result* res;
+  int begin, end;
+} bal_arg;
+
+static void* bal_worker(void* p) {
+  bal_arg* a = (bal_arg*)p;
+  for (int b = a->begin; b < a->end; ++b)
+    orc_balance_solve(a->prm, a->bp, a->recs + (size_t)b * MPCQP_BAL_SIZE, &a->res[b]);
+  return NULL;
+}
+
+int32_t orc_balance_solve_batch(const mpcqp_params* prm, const mpcqp_balance_params* bp, const double* recs,
+                                int32_t batch, mpcqp_result* res, int32_t nthreads) {
+  if (batch < 0 || !prm || !bp) return MPCQP_ERR_INVALID_ARG;
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > batch) nthreads = batch > 0 ? batch : 1;
+  pthread_t th[256];
+  bal_arg args[256];
+  if (nthreads > 256) nthreads = 256;
+  for (int t = 0; t < nthreads; ++t) {
+    args[t] = (bal_arg){prm, bp, recs, res, (int)((int64_t)batch * t / nthreads),
+                        (int)((int64_t)batch * (t + 1) / nthreads)};
+    if (nthreads == 1)
+      bal_worker(&args[t]);
+    else
+      pthread_create(&th[t], NULL, bal_worker, &args[t]);
+  }
+  if (nthreads > 1)
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   return MPCQP_OK;
 }

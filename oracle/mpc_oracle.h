@@ -80,6 +80,16 @@ void orc_joint_torques(const double* tq, const double* f_grf, int32_t* counter, 
 int32_t orc_solve_batch(const mpcqp_params* prm, const double* recs, int32_t batch,
                         mpcqp_result* res, double* sols, int32_t nthreads);
 
+/* Single-step QP balance controller (A1RobotControl.cpp:7-48, :321-332, :377-444): dense
+ * H [12][12] full symmetric, g [12], l/u [20], A [20][12] row-major from one MPCQP_BAL record. */
+void orc_balance_build_qp(const mpcqp_balance_params* bp, const double* rec, double* P, double* q,
+                          double* l, double* u, double* A);
+/* Fresh OSQP 0.6 solve of that QP with prm's settings (horizon / warm_start ignored). */
+int32_t orc_balance_solve(const mpcqp_params* prm, const mpcqp_balance_params* bp, const double* rec,
+                          mpcqp_result* res);
+int32_t orc_balance_solve_batch(const mpcqp_params* prm, const mpcqp_balance_params* bp, const double* recs,
+                                int32_t batch, mpcqp_result* res, int32_t nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -143,6 +143,11 @@ def lib():
         L.orc_solve_sequence.restype = ctypes.c_int32
         L.orc_joint_torques.argtypes = [dp, dp, ctypes.POINTER(ctypes.c_int32), dp]
         L.orc_joint_torques.restype = None
+        L.orc_balance_build_qp.argtypes = [ctypes.POINTER(BalanceParams), dp, dp, dp, dp, dp, dp]
+        L.orc_balance_build_qp.restype = None
+        L.orc_balance_solve_batch.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(BalanceParams), dp,
+                                              ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+        L.orc_balance_solve_batch.restype = ctypes.c_int32
         _lib = L
     return _lib
 
@@ -258,3 +263,38 @@ def joint_torques(tq_recs, f_grf, counters, tau):
         row = tau[b]
         lib().orc_joint_torques(_dp(tq_recs[b]), _dp(f_grf[b]), ctypes.byref(c), _dp(row))
         counters[b] = c.value
+
+
+# ---- single-step QP balance controller (A1RobotControl.cpp:7-48, :321-332, :377-444) ----------
+BAL_SIZE = 72
+
+
+class BalanceParams(ctypes.Structure):
+    """Mirror of mpcqp_balance_params (include/mpcqp.h)."""
+    _fields_ = [("q_diag", ctypes.c_double * 6), ("r", ctypes.c_double), ("mu", ctypes.c_double),
+                ("f_min", ctypes.c_double), ("f_max", ctypes.c_double)]
+
+
+def default_balance_params():
+    bp = BalanceParams()
+    for i, v in enumerate([1.0, 1.0, 1.0, 400.0, 400.0, 100.0]):
+        bp.q_diag[i] = v
+    bp.r, bp.mu, bp.f_min, bp.f_max = 1e-3, 0.7, 0.0, 180.0
+    return bp
+
+
+def balance_build_qp(bp, rec):
+    P = np.zeros((12, 12)); q = np.zeros(12); l = np.zeros(20); u = np.zeros(20); A = np.zeros((20, 12))
+    rec = np.ascontiguousarray(rec, dtype=np.float64)
+    lib().orc_balance_build_qp(ctypes.byref(bp), _dp(rec), _dp(P), _dp(q), _dp(l), _dp(u), _dp(A))
+    return P, q, l, u, A
+
+
+def balance_solve_batch(params, bp, recs, nthreads=1):
+    """Fresh OSQP solve per robot of the balance QP (params: OSQP settings; horizon ignored)."""
+    recs = np.ascontiguousarray(recs, dtype=np.float64).reshape(-1, BAL_SIZE)
+    res = np.zeros(recs.shape[0], dtype=RESULT_DTYPE)
+    rc = lib().orc_balance_solve_batch(ctypes.byref(params), ctypes.byref(bp), _dp(recs), recs.shape[0],
+                                       res.ctypes.data, nthreads)
+    assert rc == 0
+    return res

@@ -137,3 +137,39 @@ def ipm_qp(H, g, C, lo, hi, tol=1e-10, max_iter=200):
         a = 0.99 * min(step_len(s, ds), step_len(z, dz))
         x, yv, s, z = x + a * dx, yv + a * dy, s + a * ds, z + a * dz
     return x
+
+
+def balance_qp(rec, q_diag, r, mu, f_min, f_max):
+    """Independent numpy restatement of the single-step QP balance controller
+    (A1RobotControl.cpp:321-332, :377-414; constraint rows of the ctor :27-44).
+    rec is one MPCQP_BAL record (include/mpcqp.h). Returns H, g, C, lo, hi."""
+    R = rec[6:15].reshape(3, 3)
+    Rz = rec[15:24].reshape(3, 3)
+    ee = rec[39:42] - rec[36:39]
+    if ee[2] > 3.1415926 * 1.5:
+        ee[2] = rec[41] - 3.1415926 * 2 - rec[38]
+    elif ee[2] < -3.1415926 * 1.5:
+        ee[2] = rec[41] + 3.1415926 * 2 - rec[38]
+    acc = np.zeros(6)
+    acc[:3] = rec[42:45] * (rec[3:6] - rec[0:3]) + R @ (rec[45:48] * (rec[27:30] - R.T @ rec[24:27]))
+    acc[3:] = rec[48:51] * ee + rec[51:54] * (rec[33:36] - R.T @ rec[30:33])
+    acc[2] += rec[54] * 9.8
+    M = np.zeros((6, 12))
+    for i in range(4):
+        M[:3, 3 * i:3 * i + 3] = np.eye(3)
+        M[3:, 3 * i:3 * i + 3] = Rz.T @ skew(rec[55 + 3 * i:58 + 3 * i])
+    Q = np.diag(q_diag)
+    H = r * np.eye(12) + M.T @ Q @ M
+    g = -M.T @ Q @ acc
+    C = np.zeros((20, 12))
+    lo = np.zeros(20)
+    hi = np.zeros(20)
+    for i in range(4):
+        c = 1.0 if rec[67 + i] != 0 else 0.0
+        C[i, 3 * i + 2] = 1.0
+        lo[i], hi[i] = c * f_min, c * f_max
+        for k, (col, sgn) in enumerate([(0, 1.0), (0, -1.0), (1, 1.0), (1, -1.0)]):
+            C[4 + 4 * i + k, 3 * i + col] = sgn
+            C[4 + 4 * i + k, 3 * i + 2] = -mu
+            lo[4 + 4 * i + k] = -1e30
+    return H, g, C, lo, hi
