@@ -264,6 +264,14 @@ int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t 
   return MPCQP_OK;
 }
 
+int32_t mpcqp_assemble_records_device(int32_t horizon, const double* d_states, int32_t batch, double* d_records,
+                                      void* stream) {
+  if (horizon < 1 || horizon > MPCQP_MAX_HORIZON || batch < 0 || (batch > 0 && (!d_states || !d_records)))
+    return MPCQP_ERR_INVALID_ARG;
+  if (batch == 0) return MPCQP_OK;
+  return mpcqp::launch_assemble(horizon, d_states, batch, d_records, stream) == hipSuccess ? MPCQP_OK : MPCQP_ERR_HIP;
+}
+
 void mpcqp_balance_default_params(mpcqp_balance_params* p) {
   if (!p) return;
   const double q[6] = {1.0, 1.0, 1.0, 400.0, 400.0, 100.0};  // A1RobotControl.cpp:11

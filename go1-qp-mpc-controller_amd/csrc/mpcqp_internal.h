@@ -50,6 +50,9 @@ __host__ __device__ constexpr int warm_state_doubles(int N) {
 hipError_t launch_torques(const double* recs, const mpcqp_result* grf, int batch, int* counter, double* tau,
                           void* stream);
 
+// Input assembly from raw robot state (mpcqp_assemble.hip)
+hipError_t launch_assemble(int horizon, const double* states, int batch, double* recs, void* stream);
+
 // Single-step QP balance controller (mpcqp_balance.hip)
 hipError_t launch_balance(const mpcqp_balance_params& bp, const mpcqp_params& p, const double* recs, int batch,
                           mpcqp_result* out, void* stream);

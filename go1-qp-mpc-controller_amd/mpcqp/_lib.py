@@ -24,6 +24,10 @@ REC_X0, REC_EULER, REC_ROT, REC_INERTIA = 0, 13, 16, 25
 REC_MASS, REC_MU, REC_FZMIN, REC_FZMAX, REC_DT, REC_CONTACTS, REC_XREF = 34, 35, 36, 37, 38, 39, 44
 
 
+# raw robot-state row (include/mpcqp.h MPCQP_ST_*)
+ST_EULER, ST_POS, ST_ANG_VEL, ST_LIN_VEL, ST_ROT = 0, 3, 6, 9, 12
+ST_EULER_D, ST_POS_D, ST_ANG_VEL_D, ST_LIN_VEL_D, ST_FEET = 21, 24, 27, 30, 33
+ST_MASS, ST_INERTIA, ST_MU, ST_FZMIN, ST_FZMAX, ST_DT, ST_CONTACTS, ST_SIZE = 45, 46, 55, 56, 57, 58, 59, 64
 # torque-map record layout (include/mpcqp.h MPCQP_TQ_*)
 TQ_JFOOT, TQ_FKIN, TQ_KM, TQ_GRAV, TQ_CONTACTS, TQ_SIZE = 0, 36, 48, 51, 63, 68
 
@@ -97,7 +101,7 @@ EXPORTED = [
     "mpcqp_debug_solve_trace_device", "mpcqp_abi_sizes", "mpcqp_handle_slots", "mpcqp_solve_threads",
     "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_joint_torques_device",
     "mpcqp_warm_state_size", "mpcqp_solve_batch_warm_device",
-    "mpcqp_balance_default_params", "mpcqp_balance_solve_device",
+    "mpcqp_balance_default_params", "mpcqp_balance_solve_device", "mpcqp_assemble_records_device",
 ]
 
 _lib = None
@@ -160,6 +164,8 @@ def load():
     L.mpcqp_balance_default_params.restype = None
     L.mpcqp_balance_solve_device.argtypes = [vp, ctypes.POINTER(BalanceParams), vp, i32, vp, vp]
     L.mpcqp_balance_solve_device.restype = i32
+    L.mpcqp_assemble_records_device.argtypes = [i32, vp, i32, vp, vp]
+    L.mpcqp_assemble_records_device.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):
@@ -181,6 +187,12 @@ def default_params(horizon=10, **over):
         else:
             setattr(p, k, v)
     return p
+
+
+def assemble_records_device(horizon, d_states, batch, d_records, stream=0):
+    """mpcqp_assemble_records_device: raw-state rows [batch][ST_SIZE] -> MPC records, on the device."""
+    check(load().mpcqp_assemble_records_device(int(horizon), d_states, int(batch), d_records, stream or None),
+          None, "mpcqp_assemble_records_device")
 
 
 def default_balance_params(**over):

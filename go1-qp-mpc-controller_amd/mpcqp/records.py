@@ -93,6 +93,33 @@ def assemble_compute_grf(s: RobotStates, N=10):
     return rec
 
 
+def pack_states(s: RobotStates):
+    """Raw robot-state rows [B, ST_SIZE] (include/mpcqp.h MPCQP_ST_*) for the on-device assembly
+    (mpcqp_assemble_records_device), which then produces exactly assemble_compute_grf's records."""
+    from . import _lib as L
+    B = s.batch
+    st = np.zeros((B, L.ST_SIZE))
+    st[:, L.ST_EULER:L.ST_EULER + 3] = s.root_euler
+    st[:, L.ST_POS:L.ST_POS + 3] = s.root_pos
+    st[:, L.ST_ANG_VEL:L.ST_ANG_VEL + 3] = s.root_ang_vel
+    st[:, L.ST_LIN_VEL:L.ST_LIN_VEL + 3] = s.root_lin_vel
+    st[:, L.ST_ROT:L.ST_ROT + 9] = np.asarray(s.root_rot_mat, dtype=np.float64).reshape(B, 9)
+    st[:, L.ST_EULER_D:L.ST_EULER_D + 3] = s.root_euler_d
+    st[:, L.ST_POS_D:L.ST_POS_D + 3] = s.root_pos_d
+    st[:, L.ST_ANG_VEL_D:L.ST_ANG_VEL_D + 3] = s.root_ang_vel_d
+    st[:, L.ST_LIN_VEL_D:L.ST_LIN_VEL_D + 3] = s.root_lin_vel_d
+    st[:, L.ST_FEET:L.ST_FEET + 12] = np.asarray(s.foot_pos_abs, dtype=np.float64).reshape(B, 12)
+    st[:, L.ST_MASS] = GO1_MASS if s.robot_mass is None else s.robot_mass
+    inertia = GO1_INERTIA[None] if s.trunk_inertia is None else np.asarray(s.trunk_inertia)
+    st[:, L.ST_INERTIA:L.ST_INERTIA + 9] = np.broadcast_to(inertia.reshape(-1, 9), (B, 9))
+    st[:, L.ST_MU] = 0.3 if s.mu is None else s.mu
+    st[:, L.ST_FZMIN] = s.fz_min
+    st[:, L.ST_FZMAX] = s.fz_max
+    st[:, L.ST_DT] = s.mpc_dt
+    st[:, L.ST_CONTACTS:L.ST_CONTACTS + 4] = np.asarray(s.contacts, dtype=bool).astype(np.float64)
+    return st
+
+
 def assemble_test_mpc(N=10):
     """test_mpc.cpp:15-122 → (record [rec_size(N)], q_weights, r_weights)."""
     dt = 0.0025

@@ -165,6 +165,36 @@ int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t
 int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t batch,
                               double* d_P, double* d_q, double* d_l, double* d_u, void* stream);
 
+/* ---- on-device input assembly from raw robot state --------------------
+ * One binary64 record per robot holding the A1CtrlStates / Go1CtrlStates fields the MPC branch of
+ * compute_grf reads (A1RobotControl.cpp:446-514); matrices row-major, vectors world frame unless
+ * noted.  Offsets in doubles.                                                                  */
+#define MPCQP_ST_EULER 0      /* [3] root_euler                                                  */
+#define MPCQP_ST_POS 3        /* [3] root_pos                                                    */
+#define MPCQP_ST_ANG_VEL 6    /* [3] root_ang_vel (world)                                        */
+#define MPCQP_ST_LIN_VEL 9    /* [3] root_lin_vel (world)                                        */
+#define MPCQP_ST_ROT 12       /* [9] root_rot_mat                                                */
+#define MPCQP_ST_EULER_D 21   /* [3] root_euler_d (after terrain adaptation, :335-376)           */
+#define MPCQP_ST_POS_D 24     /* [3] root_pos_d                                                  */
+#define MPCQP_ST_ANG_VEL_D 27 /* [3] root_ang_vel_d                                              */
+#define MPCQP_ST_LIN_VEL_D 30 /* [3] root_lin_vel_d (body frame; :470 rotates it to world)       */
+#define MPCQP_ST_FEET 33      /* [4][3] foot_pos_abs column i                                     */
+#define MPCQP_ST_MASS 45      /* robot_mass                                                      */
+#define MPCQP_ST_INERTIA 46   /* [9] trunk_inertia                                               */
+#define MPCQP_ST_MU 55        /* friction coefficient (ConvexMpc.cpp:8: 0.3)                      */
+#define MPCQP_ST_FZMIN 56     /* 0                                                               */
+#define MPCQP_ST_FZMAX 57     /* 180                                                             */
+#define MPCQP_ST_DT 58        /* mpc_dt (:462, 0.0025)                                           */
+#define MPCQP_ST_CONTACTS 59  /* [4] contacts[i] as 0.0 / 1.0                                    */
+#define MPCQP_ST_SIZE 64      /* 63 used, padded to a multiple of 4 doubles                      */
+
+/* Replaces the host-side x0 / x_ref / horizon-feet assembly of compute_grf (A1RobotControl.cpp:
+ * 452-514: mpc_states, root_lin_vel_d_world, mpc_states_d, B_mat_d_list feet) for `batch` robots:
+ * d_states [batch][MPCQP_ST_SIZE] -> d_records [batch][mpcqp_record_size(horizon)], DEVICE
+ * pointers, async on `stream`.  Chain it before mpcqp_solve_batch_device on the same stream. */
+int32_t mpcqp_assemble_records_device(int32_t horizon, const double* d_states, int32_t batch, double* d_records,
+                                      void* stream);
+
 /* ---- downstream torque map: A1RobotControl::compute_joint_torques (A1RobotControl.cpp:289-319)
  * One binary64 record per robot (offsets in doubles); FL, FR, RL, RR leg order.             */
 #define MPCQP_TQ_JFOOT 0      /* [4][9] j_foot.block<3,3>(3i,3i), row-major (A1CtrlStates.h:410) */

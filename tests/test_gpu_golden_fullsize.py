@@ -11,7 +11,8 @@ from gpu_helpers import rel_err_u0, solve_gpu
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SETS = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+# balance.npz is the balance controller's set (tests/test_balance.py, tests/test_gpu_balance.py)
+SETS = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endswith("balance.npz"))
 
 
 @pytest.mark.parametrize("path", SETS, ids=[os.path.basename(p) for p in SETS])

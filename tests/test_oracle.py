@@ -10,7 +10,8 @@ import mpcqp
 import numpy_reference as nr
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SETS = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+# balance.npz is the balance controller's set (tests/test_balance.py, tests/test_gpu_balance.py)
+SETS = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endswith("balance.npz"))
 
 
 def test_golden_sets_present():
