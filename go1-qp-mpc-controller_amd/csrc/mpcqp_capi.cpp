@@ -28,6 +28,9 @@ struct mpcqp_handle {
   mpcqp_result* d_res = nullptr;
   double* d_sol = nullptr;
   size_t cap = 0;
+  double* d_bal_recs = nullptr;  // balance host wrapper staging
+  mpcqp_result* d_bal_res = nullptr;
+  size_t bal_cap = 0;
   char err[256] = {0};
 };
 
@@ -157,6 +160,8 @@ int32_t mpcqp_destroy(mpcqp_handle* h) {
   (void)hipFree(h->d_recs);
   (void)hipFree(h->d_res);
   (void)hipFree(h->d_sol);
+  (void)hipFree(h->d_bal_recs);
+  (void)hipFree(h->d_bal_res);
   delete h;
   return MPCQP_OK;
 }
@@ -290,6 +295,30 @@ int32_t mpcqp_balance_solve_device(mpcqp_handle* h, const mpcqp_balance_params* 
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
   e = mpcqp::launch_balance(*bp, h->p, d_records, batch, d_results, stream);
   if (e != hipSuccess) return set_hip_error(h, e, "balance_kernel launch");
+  return MPCQP_OK;
+}
+
+int32_t mpcqp_balance_solve_host(mpcqp_handle* h, const mpcqp_balance_params* bp, const double* h_records,
+                                 int32_t batch, mpcqp_result* h_results) {
+  if (!h || !bp || batch < 0 || (batch > 0 && (!h_records || !h_results))) return MPCQP_ERR_INVALID_ARG;
+  if (batch == 0) return MPCQP_OK;
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
+  if ((size_t)batch > h->bal_cap) {
+    (void)hipFree(h->d_bal_recs);
+    (void)hipFree(h->d_bal_res);
+    h->d_bal_recs = nullptr; h->d_bal_res = nullptr; h->bal_cap = 0;
+    e = hipMalloc(&h->d_bal_recs, sizeof(double) * MPCQP_BAL_SIZE * batch);
+    if (e == hipSuccess) e = hipMalloc(&h->d_bal_res, sizeof(mpcqp_result) * batch);
+    if (e != hipSuccess) return set_hip_error(h, e, "hipMalloc");
+    h->bal_cap = batch;
+  }
+  e = hipMemcpy(h->d_bal_recs, h_records, sizeof(double) * MPCQP_BAL_SIZE * batch, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipMemcpy H2D");
+  int32_t rc = mpcqp_balance_solve_device(h, bp, h->d_bal_recs, batch, h->d_bal_res, nullptr);
+  if (rc != MPCQP_OK) return rc;
+  e = hipMemcpy(h_results, h->d_bal_res, sizeof(mpcqp_result) * batch, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return set_hip_error(h, e, "hipMemcpy D2H");
   return MPCQP_OK;
 }
 

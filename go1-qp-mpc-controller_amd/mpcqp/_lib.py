@@ -102,6 +102,7 @@ EXPORTED = [
     "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_joint_torques_device",
     "mpcqp_warm_state_size", "mpcqp_solve_batch_warm_device",
     "mpcqp_balance_default_params", "mpcqp_balance_solve_device", "mpcqp_assemble_records_device",
+    "mpcqp_balance_solve_host",
 ]
 
 _lib = None
@@ -164,6 +165,8 @@ def load():
     L.mpcqp_balance_default_params.restype = None
     L.mpcqp_balance_solve_device.argtypes = [vp, ctypes.POINTER(BalanceParams), vp, i32, vp, vp]
     L.mpcqp_balance_solve_device.restype = i32
+    L.mpcqp_balance_solve_host.argtypes = [vp, ctypes.POINTER(BalanceParams), dp, i32, vp]
+    L.mpcqp_balance_solve_host.restype = i32
     L.mpcqp_assemble_records_device.argtypes = [i32, vp, i32, vp, vp]
     L.mpcqp_assemble_records_device.restype = i32
     ps, rs = i32(0), i32(0)

@@ -254,6 +254,9 @@ void mpcqp_balance_default_params(mpcqp_balance_params* p);
  * guard in this branch, :440-443: a NaN solution stays NaN and sets nan_legs). */
 int32_t mpcqp_balance_solve_device(mpcqp_handle* h, const mpcqp_balance_params* bp, const double* d_records,
                                    int32_t batch, mpcqp_result* d_results, void* stream);
+/* Host-pointer convenience wrapper of the above (copies in, solves, copies out, synchronizes). */
+int32_t mpcqp_balance_solve_host(mpcqp_handle* h, const mpcqp_balance_params* bp, const double* h_records,
+                                 int32_t batch, mpcqp_result* h_results);
 
 const char* mpcqp_status_str(int32_t status);
 const char* mpcqp_error_str(int32_t err);

@@ -276,12 +276,75 @@ class RobotControlT {
       for (int l = 0; l < 4; ++l) foot_forces_grf(r, l) = f[r * 4 + l];
   }
 
+  // ---- stance_leg_control_type == 0: single-step QP balance controller -----------------------
+  // A1RobotControl ctor constants (:11-15); a caller may edit them before the first call.
+  mpcqp_balance_params balance_params = [] {
+    mpcqp_balance_params p;
+    mpcqp_balance_default_params(&p);
+    return p;
+  }();
+
+  // A1RobotControl.cpp:321-332 + :377-414 inputs of one robot -> MPCQP_BAL record
+  template <class State>
+  static void assemble_balance(const State& s, double* rec) {
+    std::memset(rec, 0, sizeof(double) * MPCQP_BAL_SIZE);
+    for (int k = 0; k < 3; ++k) {
+      rec[MPCQP_BAL_POS + k] = s.root_pos[k];
+      rec[MPCQP_BAL_POS_D + k] = s.root_pos_d[k];
+      rec[MPCQP_BAL_LIN_VEL + k] = s.root_lin_vel[k];
+      rec[MPCQP_BAL_LIN_VEL_D + k] = s.root_lin_vel_d[k];
+      rec[MPCQP_BAL_ANG_VEL + k] = s.root_ang_vel[k];
+      rec[MPCQP_BAL_ANG_VEL_D + k] = s.root_ang_vel_d[k];
+      rec[MPCQP_BAL_EULER + k] = s.root_euler[k];
+      rec[MPCQP_BAL_EULER_D + k] = s.root_euler_d[k];
+      rec[MPCQP_BAL_KP_LIN + k] = s.kp_linear[k];
+      rec[MPCQP_BAL_KD_LIN + k] = s.kd_linear[k];
+      rec[MPCQP_BAL_KP_ANG + k] = s.kp_angular[k];
+      rec[MPCQP_BAL_KD_ANG + k] = s.kd_angular[k];
+    }
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        rec[MPCQP_BAL_ROT + 3 * r + c] = s.root_rot_mat(r, c);
+        rec[MPCQP_BAL_ROT_Z + 3 * r + c] = s.root_rot_mat_z(r, c);
+      }
+    rec[MPCQP_BAL_MASS] = s.robot_mass;
+    for (int l = 0; l < 4; ++l) {
+      for (int r = 0; r < 3; ++r) rec[MPCQP_BAL_FEET + 3 * l + r] = s.foot_pos_abs(r, l);
+      rec[MPCQP_BAL_CONTACTS + l] = s.contacts[l] ? 1.0 : 0.0;
+    }
+  }
+
+  // Batched QP branch of compute_grf: forces[b] = foot_forces_grf (row r / leg l at [r*4+l]).
+  template <class State>
+  void compute_grf_qp_batch(const State* states, int count, double* forces, mpcqp_result* results = nullptr) {
+    bal_recs_.resize((size_t)count * MPCQP_BAL_SIZE);
+    res_.resize(count);
+    for (int b = 0; b < count; ++b) assemble_balance(states[b], &bal_recs_[(size_t)b * MPCQP_BAL_SIZE]);
+    throw_on(mpcqp_balance_solve_host(h_, &balance_params, bal_recs_.data(), count, res_.data()), h_,
+             "mpcqp_balance_solve_host");
+    for (int b = 0; b < count; ++b) {
+      for (int l = 0; l < 4; ++l)
+        for (int r = 0; r < 3; ++r) forces[(size_t)b * 12 + r * 4 + l] = res_[b].f_body[3 * l + r];
+      if (results) results[b] = res_[b];
+    }
+  }
+
+  // A1RobotControl::compute_grf with state.stance_leg_control_type == 0 (:377-444)
+  template <class State, class Mat34>
+  void compute_grf_qp(const State& state, Mat34& foot_forces_grf) {
+    double f[12];
+    compute_grf_qp_batch(&state, 1, f);
+    for (int r = 0; r < 3; ++r)
+      for (int l = 0; l < 4; ++l) foot_forces_grf(r, l) = f[r * 4 + l];
+  }
+
   mpcqp_handle* handle() const { return h_; }
 
  private:
   mpcqp_params params_{};
   mpcqp_handle* h_ = nullptr;
   std::vector<double> recs_;
+  std::vector<double> bal_recs_;
   std::vector<mpcqp_result> res_;
 };
 

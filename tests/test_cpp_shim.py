@@ -54,3 +54,26 @@ def test_cpp_test_mpc_harness(oracle):
     f = np.array(grf)  # 3x4 body frame
     fr = np.array(ref2["f_body"]).reshape(4, 3).T
     assert np.max(np.abs(f - fr)) <= 1e-4 * max(np.max(np.abs(fr)), 1)
+
+
+@pytest.mark.gpu
+def test_cpp_balance_branch(oracle):
+    """compute_grf_qp (stance_leg_control_type == 0) through the C++ shim == oracle balance solve."""
+    exe = os.path.join(REPO, "tests", "cpp", "build", "test_balance_gpu")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(REPO, "tests", "cpp")], check=True)
+    out = subprocess.run([exe], check=True, capture_output=True, text=True, timeout=120).stdout
+    grf, rec, st = [], None, None
+    for line in out.splitlines():
+        parts = line.split()
+        if parts[0] == "REC":
+            rec = np.array([float(x) for x in parts[1:]])
+        elif parts[0] == "GRF":
+            grf.append([float(x) for x in parts[1:]])
+        elif parts[0] == "STATUS":
+            st = (int(parts[1]), int(parts[3]))
+    ref = oracle.balance_solve_batch(oracle.default_params(1), oracle.default_balance_params(), rec[None])[0]
+    assert st == (int(ref["status"]), int(ref["iters"]))
+    fr = np.array(ref["f_body"]).reshape(4, 3).T
+    np.testing.assert_array_equal(np.array(grf), fr)
+    assert fr[2, 0] > 20 and fr[2, 3] > 20 and np.all(np.abs(fr[:, 1:3]) < 1e-6)
