@@ -3,7 +3,7 @@
 
 Collect in its own pass (no --sys-trace / --runtime-trace with --pmc):
 
-  rocprofv3 --pmc FETCH_SIZE --kernel-include-regex solve_kernel --output-format csv \\
+  rocprofv3 --pmc FETCH_SIZE --kernel-include-regex wave_kernel --output-format csv \\
       -d gpurun_out/pmc/fetch -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu
   rocprofv3 --pmc WRITE_SIZE ... -d gpurun_out/pmc/write ...   (FETCH_SIZE and WRITE_SIZE do not
                                                                fit one pass on gfx950's TCC)
@@ -47,7 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--key", default="N10_B4096_trot")
-    ap.add_argument("--kernel", default="solve_kernel")
+    ap.add_argument("--kernel", default="wave_kernel")  # the default path's kernel
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     per, names = parse(a.dir, a.kernel)
