@@ -36,6 +36,22 @@ struct mpcqp_handle {
 
 namespace {
 
+// Makes the handle's device current for one entry point and restores the caller's current device
+// on every return path (a multi-GPU caller such as torch keeps its own device selection).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err;
+  explicit DeviceGuard(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    err = hipSetDevice(device);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 int set_hip_error(mpcqp_handle* h, hipError_t e, const char* where) {
   if (h) snprintf(h->err, sizeof(h->err), "%s: %s", where, hipGetErrorString(e));
   return MPCQP_ERR_HIP;
@@ -140,7 +156,8 @@ int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** 
   if (!h) return MPCQP_ERR_ALLOC;
   h->p = *params;
   h->device = device;
-  hipError_t e = hipSetDevice(device);
+  DeviceGuard dg(device);
+  hipError_t e = dg.err;
   if (e != hipSuccess) { delete h; return MPCQP_ERR_HIP; }
   int cus = 0, per_cu = 0;
   e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -155,7 +172,7 @@ int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** 
 
 int32_t mpcqp_destroy(mpcqp_handle* h) {
   if (!h) return MPCQP_ERR_INVALID_ARG;
-  (void)hipSetDevice(h->device);
+  DeviceGuard dg(h->device);
   (void)hipFree(h->work);
   (void)hipFree(h->d_recs);
   (void)hipFree(h->d_res);
@@ -172,7 +189,8 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   if (!h || batch < 0 || (batch > 0 && (!d_records || !d_results))) return MPCQP_ERR_INVALID_ARG;
   if (d_state && effective_path(h) != 3) return MPCQP_ERR_INVALID_ARG;  // warm start: wave path only
   if (batch == 0) return MPCQP_OK;
-  hipError_t e = hipSetDevice(h->device);
+  DeviceGuard dg(h->device);
+  hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
   // grow-only; a capture-safe caller pre-sizes with mpcqp_reserve()
   e = ensure_workspace(h, batch, stream);
@@ -224,7 +242,8 @@ int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t
                                mpcqp_result* h_results, double* h_solution) {
   if (!h || batch < 0 || (batch > 0 && (!h_records || !h_results))) return MPCQP_ERR_INVALID_ARG;
   if (batch == 0) return MPCQP_OK;
-  hipError_t e = hipSetDevice(h->device);
+  DeviceGuard dg(h->device);
+  hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
   const size_t rs = (size_t)MPCQP_REC_SIZE(h->p.horizon);
   const size_t n = (size_t)MPCQP_NUM_DOF * h->p.horizon;
@@ -256,7 +275,8 @@ int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t 
   if (!h || batch < 0 || (batch > 0 && (!d_records || !d_P || !d_q || !d_l || !d_u)))
     return MPCQP_ERR_INVALID_ARG;
   if (batch == 0) return MPCQP_OK;
-  hipError_t e = hipSetDevice(h->device);
+  DeviceGuard dg(h->device);
+  hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
   mpcqp::LaunchArgs a;
   memset(&a, 0, sizeof(a));
@@ -291,7 +311,8 @@ int32_t mpcqp_balance_solve_device(mpcqp_handle* h, const mpcqp_balance_params* 
                                    int32_t batch, mpcqp_result* d_results, void* stream) {
   if (!h || !bp || batch < 0 || (batch > 0 && (!d_records || !d_results))) return MPCQP_ERR_INVALID_ARG;
   if (batch == 0) return MPCQP_OK;
-  hipError_t e = hipSetDevice(h->device);
+  DeviceGuard dg(h->device);
+  hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
   e = mpcqp::launch_balance(*bp, h->p, d_records, batch, d_results, stream);
   if (e != hipSuccess) return set_hip_error(h, e, "balance_kernel launch");
@@ -302,7 +323,8 @@ int32_t mpcqp_balance_solve_host(mpcqp_handle* h, const mpcqp_balance_params* bp
                                  int32_t batch, mpcqp_result* h_results) {
   if (!h || !bp || batch < 0 || (batch > 0 && (!h_records || !h_results))) return MPCQP_ERR_INVALID_ARG;
   if (batch == 0) return MPCQP_OK;
-  hipError_t e = hipSetDevice(h->device);
+  DeviceGuard dg(h->device);
+  hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
   if ((size_t)batch > h->bal_cap) {
     (void)hipFree(h->d_bal_recs);
@@ -371,7 +393,8 @@ int32_t mpcqp_handle_slots(mpcqp_handle* h) { return h ? h->slots : 0; }
 
 int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {
   if (!h || batch < 0) return MPCQP_ERR_INVALID_ARG;
-  hipError_t e = hipSetDevice(h->device);
+  DeviceGuard dg(h->device);
+  hipError_t e = dg.err;
   if (e == hipSuccess && ((size_t)batch > h->work_cap || work_per_instance(h) > h->work_per))
     e = hipDeviceSynchronize();
   if (e == hipSuccess) e = ensure_workspace(h, batch, nullptr);
@@ -387,7 +410,8 @@ int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
   if (!h || path < 0 || path > 3) return MPCQP_ERR_INVALID_ARG;
   if (path == 1 && h->p.horizon > mpcqp::DENSE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
   if (path == 3 && h->p.horizon > mpcqp::WAVE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
-  hipError_t e = hipSetDevice(h->device);
+  DeviceGuard dg(h->device);
+  hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
   const int old = h->path;
   h->path = path;

@@ -50,11 +50,12 @@ struct Cfg {
 // Warm-start slot of one robot (binary64, caller-owned device memory): everything the reference's
 // persistent OsqpEigen solver carries from one tick to the next.  Scaled quantities are stored as
 // the kernel used them; the zero pattern of H's upper triangle (one bit per entry, MW words per
-// column) decides between osqp_update_P and OsqpEigen's re-init on the next tick.
+// column) and the friction coefficient mu the constraint matrix was built with decide between
+// osqp_update_P and OsqpEigen's re-init on the next tick.
 template <int N>
 struct WarmLayout {
   static constexpr int n = ND * N, m = CD * N, MW = (n + 63) / 64;
-  static constexpr int FLAG = 0, RHO = 1, C = 2, D = 4, E = D + n, QT = E + m, AK = QT + n, X = AK + 2 * m,
+  static constexpr int FLAG = 0, RHO = 1, C = 2, MU = 3, D = 4, E = D + n, QT = E + m, AK = QT + n, X = AK + 2 * m,
                        Z = X + n, Y = Z + m, MASK = Y + m, SIZE = MASK + MW * n;
   static_assert(SIZE == warm_state_doubles(N), "warm-start slot layout");
 };
@@ -769,7 +770,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   // old scaling, rescale with the previous A and q, keep iterates and rho); a changed pattern ->
   // re-init (fresh scaling and rho) with the previous unscaled x, y restored (oracle ws_update).
   const bool pattern_changed = (p.scaling > 0 || ws) ? colmax(cm, ws != nullptr) : false;
-  const int mode = !had ? 0 : (pattern_changed ? 2 : 1);  // 0 cold, 1 update_P, 2 re-init
+  // A is set once per solver init (A1RobotControl.cpp:526-530); a robot whose mu changed gets a
+  // re-init with the new friction cone rather than update_P on the old one (oracle ws_update).
+  const bool mu_changed = had && ws[WL::MU] != mu;
+  const int mode = !had ? 0 : ((pattern_changed || mu_changed) ? 2 : 1);  // 0 cold, 1 update_P, 2 re-init
   if (mode == 1) {
     // unscale_data with the previous scaling: q = D^-1 (c^-1 q~), A = (E^-1 A~) D^-1
     const double cinv_o = 1. / ws[WL::C];
@@ -1316,6 +1320,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       ws[WL::FLAG] = 1.0;
       ws[WL::RHO] = rho;
       ws[WL::C] = cost_c;
+      ws[WL::MU] = mu;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {

@@ -53,7 +53,10 @@ class ConvexMpc {
     linear_constraints.assign((size_t)m * n, 0.0);
     reset();
   }
-  ~ConvexMpc() { if (h_) mpcqp_destroy(h_); }
+  ~ConvexMpc() {
+    free_device();
+    if (h_) mpcqp_destroy(h_);
+  }
   ConvexMpc(const ConvexMpc&) = delete;
   ConvexMpc& operator=(const ConvexMpc&) = delete;
 
@@ -134,8 +137,11 @@ class ConvexMpc {
 
  private:
   void build_on_device();
+  void free_device();
   mpcqp_params params_{};
   mpcqp_handle* h_ = nullptr;
+  // device staging of build_on_device, allocated on first use and owned by the object
+  double *d_rec_ = nullptr, *d_P_ = nullptr, *d_q_ = nullptr, *d_l_ = nullptr, *d_u_ = nullptr;
   std::vector<double> rec_;
   double pending_feet_[12] = {0};
   int step_ = 0;
@@ -148,27 +154,38 @@ class ConvexMpc {
 namespace mpcqp_cpp {
 
 template <int N>
+void ConvexMpc<N>::free_device() {
+  (void)hipFree(d_rec_);
+  (void)hipFree(d_P_);
+  (void)hipFree(d_q_);
+  (void)hipFree(d_l_);
+  (void)hipFree(d_u_);
+  d_rec_ = d_P_ = d_q_ = d_l_ = d_u_ = nullptr;
+}
+
+template <int N>
 void ConvexMpc<N>::build_on_device() {
-  double *d_rec = nullptr, *d_P = nullptr, *d_q = nullptr, *d_l = nullptr, *d_u = nullptr;
   auto ok = [&](hipError_t e) {
     if (e != hipSuccess) throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e));
   };
-  ok(hipMalloc(&d_rec, sizeof(double) * rec_.size()));
-  ok(hipMalloc(&d_P, sizeof(double) * hessian.size()));
-  ok(hipMalloc(&d_q, sizeof(double) * n));
-  ok(hipMalloc(&d_l, sizeof(double) * m));
-  ok(hipMalloc(&d_u, sizeof(double) * m));
-  ok(hipMemcpy(d_rec, rec_.data(), sizeof(double) * rec_.size(), hipMemcpyHostToDevice));
-  throw_on(mpcqp_build_qp_device(h_, d_rec, 1, d_P, d_q, d_l, d_u, nullptr), h_, "mpcqp_build_qp_device");
-  ok(hipMemcpy(hessian.data(), d_P, sizeof(double) * hessian.size(), hipMemcpyDeviceToHost));
-  ok(hipMemcpy(gradient.data(), d_q, sizeof(double) * n, hipMemcpyDeviceToHost));
-  ok(hipMemcpy(lb.data(), d_l, sizeof(double) * m, hipMemcpyDeviceToHost));
-  ok(hipMemcpy(ub.data(), d_u, sizeof(double) * m, hipMemcpyDeviceToHost));
-  (void)hipFree(d_rec);
-  (void)hipFree(d_P);
-  (void)hipFree(d_q);
-  (void)hipFree(d_l);
-  (void)hipFree(d_u);
+  if (!d_u_) {  // first call: all five buffers or none (a failed allocation frees the others)
+    try {
+      ok(hipMalloc(&d_rec_, sizeof(double) * rec_.size()));
+      ok(hipMalloc(&d_P_, sizeof(double) * hessian.size()));
+      ok(hipMalloc(&d_q_, sizeof(double) * n));
+      ok(hipMalloc(&d_l_, sizeof(double) * m));
+      ok(hipMalloc(&d_u_, sizeof(double) * m));
+    } catch (...) {
+      free_device();
+      throw;
+    }
+  }
+  ok(hipMemcpy(d_rec_, rec_.data(), sizeof(double) * rec_.size(), hipMemcpyHostToDevice));
+  throw_on(mpcqp_build_qp_device(h_, d_rec_, 1, d_P_, d_q_, d_l_, d_u_, nullptr), h_, "mpcqp_build_qp_device");
+  ok(hipMemcpy(hessian.data(), d_P_, sizeof(double) * hessian.size(), hipMemcpyDeviceToHost));
+  ok(hipMemcpy(gradient.data(), d_q_, sizeof(double) * n, hipMemcpyDeviceToHost));
+  ok(hipMemcpy(lb.data(), d_l_, sizeof(double) * m, hipMemcpyDeviceToHost));
+  ok(hipMemcpy(ub.data(), d_u_, sizeof(double) * m, hipMemcpyDeviceToHost));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -197,14 +214,20 @@ class RobotControlT {
   RobotControlT& operator=(const RobotControlT&) = delete;
 
   double mpc_dt = 0.0025;  // A1RobotControl.cpp:462
+  // The reference's ROS param `use_sim_time` (read at A1RobotControl.cpp:63): when true, the MPC
+  // horizon uses the caller's dt instead of mpc_dt (:464-467).
+  bool use_sim_time = false;
   double mu = 0.3, fz_min = 0.0, fz_max = 180.0;
 
   // A1RobotControl.cpp:452-514: mutates state.mpc_states / mpc_states_d / root_lin_vel_d_world
   // exactly like the reference, and writes the record for the solve.
   template <class State>
   void assemble(State& s, double* rec) const {
+    assemble(s, rec, mpc_dt);
+  }
+  template <class State>
+  void assemble(State& s, double* rec, double dt) const {
     std::memset(rec, 0, sizeof(double) * MPCQP_REC_SIZE(N));
-    const double dt = mpc_dt;
     double x0[13];
     for (int k = 0; k < 3; ++k) {
       x0[k] = s.root_euler[k];
@@ -253,11 +276,14 @@ class RobotControlT {
   }
 
   // Batched compute_grf: forces[b] receives foot_forces_grf (3x4, row r / leg l at [r*4+l]).
+  // `dt` is the caller's thread period; it is the horizon step only when use_sim_time is set.
   template <class State>
-  void compute_grf_batch(State* states, int count, double* forces, mpcqp_result* results = nullptr) {
+  void compute_grf_batch(State* states, int count, double* forces, mpcqp_result* results = nullptr,
+                         double dt = 0.0) {
+    const double hdt = use_sim_time ? dt : mpc_dt;  // A1RobotControl.cpp:462-467
     recs_.resize((size_t)count * MPCQP_REC_SIZE(N));
     res_.resize(count);
-    for (int b = 0; b < count; ++b) assemble(states[b], &recs_[(size_t)b * MPCQP_REC_SIZE(N)]);
+    for (int b = 0; b < count; ++b) assemble(states[b], &recs_[(size_t)b * MPCQP_REC_SIZE(N)], hdt);
     throw_on(mpcqp_solve_batch_host(h_, recs_.data(), count, res_.data(), nullptr), h_, "mpcqp_solve_batch_host");
     for (int b = 0; b < count; ++b) {
       for (int l = 0; l < 4; ++l)
@@ -266,12 +292,12 @@ class RobotControlT {
     }
   }
 
-  // A1RobotControl::compute_grf(state, dt) — single robot; `dt` is ignored exactly like the
-  // reference's hardware path (mpc_dt = 0.0025 unless use_sim_time, :458-467).
+  // A1RobotControl::compute_grf(state, dt) — single robot; like the reference, the horizon step is
+  // mpc_dt = 0.0025 on hardware and `dt` when use_sim_time is set (:458-467).
   template <class State, class Mat34>
-  void compute_grf(State& state, double /*dt*/, Mat34& foot_forces_grf) {
+  void compute_grf(State& state, double dt, Mat34& foot_forces_grf) {
     double f[12];
-    compute_grf_batch(&state, 1, f);
+    compute_grf_batch(&state, 1, f, nullptr, dt);
     for (int r = 0; r < 3; ++r)
       for (int l = 0; l < 4; ++l) foot_forces_grf(r, l) = f[r * 4 + l];
   }

@@ -391,6 +391,7 @@ typedef struct {
   /* info */
   int iter, status, rho_updates;
   double pri_res, dua_res, obj_val;
+  double mu; /* friction coefficient of the constraint matrix A latched by the last setup */
 } osqp_ws;
 
 static csc dense_to_csc_upper(const double* M, int n) {
@@ -1012,6 +1013,7 @@ static void ws_free(osqp_ws* w) {
  * data copy, bound clipping, scale_data, set_rho_vec, KKT factorization; x = z = y = 0. */
 static int ws_setup_dense(osqp_ws* w, double* Pd, double* Ad);
 static int ws_setup(osqp_ws* w, const double* rec) {
+  w->mu = rec[MPCQP_REC_MU];
   const int n = w->n, m = w->m;
   double* Pd = (double*)malloc(sizeof(double) * (size_t)n * n);
   double* Ad = (double*)malloc(sizeof(double) * (size_t)m * n);
@@ -1232,7 +1234,11 @@ static int ws_update(osqp_ws* w, const double* rec) {
   orc_build_qp(w->st, rec, Pd, qn, ln, un, NULL);
   int fail = 0;
   csc Pn = dense_to_csc_upper(Pd, n);
-  int same = Pn.p[n] == w->P.p[n];
+  /* The reference sets the constraint matrix once, at initSolver (A1RobotControl.cpp:526-530), with
+   * ConvexMpc's fixed mu = 0.3 (ConvexMpc.cpp:8).  mu is a per-record input here, so a changed mu
+   * is treated like a changed Hessian pattern: the solver is re-initialized with the new A (the
+   * update_P branch would otherwise keep the old, latched cone). */
+  int same = Pn.p[n] == w->P.p[n] && rec[MPCQP_REC_MU] == w->mu;
   for (int j = 0; same && j <= n; ++j) same = Pn.p[j] == w->P.p[j];
   for (int k = 0; same && k < Pn.p[n]; ++k) same = Pn.i[k] == w->P.i[k];
   if (same) {

@@ -114,5 +114,14 @@ int main() {
     for (int l = 0; l < 4; ++l) std::printf(" %.17g", forces(r, l));
     std::printf("\n");
   }
+  // Gazebo: use_sim_time makes the horizon step the caller's dt (A1RobotControl.cpp:464-467)
+  ctrl.use_sim_time = true;
+  Mat forces_sim;
+  ctrl.compute_grf(state, 0.004, forces_sim);
+  for (int r = 0; r < 3; ++r) {
+    std::printf("GRFSIM");
+    for (int l = 0; l < 4; ++l) std::printf(" %.17g", forces_sim(r, l));
+    std::printf("\n");
+  }
   return 0;
 }

@@ -18,13 +18,15 @@ def test_cpp_test_mpc_harness(oracle):
         subprocess.run(["make", "-C", os.path.join(REPO, "tests", "cpp")], check=True)
     out = subprocess.run([EXE], check=True, capture_output=True, text=True, timeout=120).stdout
     kv = {}
-    rows, grf = [], []
+    rows, grf, grf_sim = [], [], []
     for line in out.splitlines():
         parts = line.split()
         if parts[0] == "ROW":
             rows.append([float(x) for x in parts[1:]])
         elif parts[0] == "GRF":
             grf.append([float(x) for x in parts[1:]])
+        elif parts[0] == "GRFSIM":
+            grf_sim.append([float(x) for x in parts[1:]])
         elif parts[0] == "STATUS":
             kv["status"], kv["iters"], kv["rho_updates"] = int(parts[1]), int(parts[3]), int(parts[5])
         else:
@@ -54,6 +56,13 @@ def test_cpp_test_mpc_harness(oracle):
     f = np.array(grf)  # 3x4 body frame
     fr = np.array(ref2["f_body"]).reshape(4, 3).T
     assert np.max(np.abs(f - fr)) <= 1e-4 * max(np.max(np.abs(fr)), 1)
+    # use_sim_time: the horizon step is the caller's dt (0.004), not mpc_dt
+    s.mpc_dt = 0.004
+    ref3, _ = oracle.solve(op, oracle.assemble_compute_grf(s, 10))
+    fs = np.array(grf_sim)
+    fr3 = np.array(ref3["f_body"]).reshape(4, 3).T
+    assert np.max(np.abs(fs - fr3)) <= 1e-4 * max(np.max(np.abs(fr3)), 1)
+    assert np.max(np.abs(fr3 - fr)) > 1e-3  # dt matters, so the check can see it
 
 
 @pytest.mark.gpu

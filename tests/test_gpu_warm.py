@@ -100,3 +100,23 @@ def test_warm_nan_tick_leaves_state(oracle):
     assert got[2]["status"][3] == mpcqp._lib.STATUS_NAN_INPUT
     ref = _oracle_sequence(oracle, p, bad)
     _check(got, ref, "nan tick")
+
+
+def test_warm_mu_change_reinit(oracle):
+    """A robot whose friction coefficient changes between ticks is re-initialized with the new
+    friction cone (the update_P branch keeps the constraint matrix of the last init)."""
+    T, B, N = 6, 32, 10
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=17, gait="stance")
+    recs_t = np.stack([mpcqp.assemble_compute_grf(s, N) for s in ticks])
+    mu = np.full((T, B), 0.6)
+    mu[3:, ::2] = 0.3  # every other robot loses friction from tick 3 on
+    recs_t[:, :, mpcqp._lib.REC_MU] = mu
+    p = mpcqp.default_params(N)
+    got = _gpu_sequence(p, recs_t)
+    ref = _oracle_sequence(oracle, p, recs_t)
+    _check(got, ref, "mu change", min_iter_equal=1.0)
+    # the solution of a tick after the change respects the new (tighter) cone
+    u = got[4]["u0"][::2].reshape(-1, 4, 3)
+    fz = u[:, :, 2]
+    tol = 0.25  # OSQP primal tolerance (test_oracle.test_solution_respects_friction_pyramid)
+    assert np.all(np.abs(u[:, :, :2]).max(-1) <= 0.3 * fz + tol)

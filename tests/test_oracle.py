@@ -72,6 +72,26 @@ def test_solution_respects_friction_pyramid(oracle):
         assert np.all(x[:, 2] >= -tol) and np.all(x[:, 2] <= 180 * c + tol)
 
 
+def test_warm_mu_change_uses_new_cone(oracle):
+    """The persistent solver re-initializes when a robot's mu changes: the warm-started solve of a
+    later tick obeys the new, tighter friction cone (with mu latched it would keep the old one)."""
+    T, B, N = 6, 32, 10
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=17, gait="stance")
+    recs = np.stack([mpcqp.assemble_compute_grf(s, N) for s in ticks])
+    p = oracle.default_params(N)
+    ratios = {}
+    for mu_late in (0.9, 0.3):
+        recs[:, :, mpcqp._lib.REC_MU] = 0.9
+        recs[3:, :, mpcqp._lib.REC_MU] = mu_late
+        res = oracle.solve_sequence(p, recs, nthreads=4)
+        assert np.all(res["status"] == 1)
+        u = res[4]["u0"].reshape(-1, 4, 3)
+        big = u[:, :, 2] > 10.0
+        ratios[mu_late] = (np.abs(u[:, :, :2]).max(-1)[big] / u[:, :, 2][big]).max()
+    assert ratios[0.9] > 0.8  # the cone binds for these states, so the test can see mu
+    assert ratios[0.3] <= 0.3 * (1 + 1e-2)
+
+
 def test_all_swing_gives_zero_forces():
     d = np.load(os.path.join(GOLDEN, "edge.npz"))
     assert np.all(np.abs(d["u0"][0]) <= 1e-6)
