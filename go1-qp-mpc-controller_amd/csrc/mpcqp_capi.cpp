@@ -81,7 +81,7 @@ size_t work_per_instance(const mpcqp_handle* h) {
   switch (effective_path(h)) {
     case 1: return mpcqp::workspace_doubles(h->p.horizon);
     case 2: return mpcqp::riccati_workspace_doubles(h->p.horizon);
-    default: return 0;  // the wave kernel keeps everything on chip
+    default: return mpcqp::scale_image_doubles(h->p.horizon);  // scale_kernel -> wave_kernel hand-off
   }
 }
 hipError_t occupancy_for(const mpcqp_handle* h, int* per_cu) {

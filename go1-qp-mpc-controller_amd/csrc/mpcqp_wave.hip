@@ -482,6 +482,440 @@ __device__ void factorize(WSmem<N>& sm, const mpcqp_params& p, const Adisc& A, d
   }
 }
 
+// ---- OSQP scale_data (scaling.c) as a kernel of its own -------------------------------------------
+// Ruiz equilibration is embarrassingly parallel over the columns of P~ = c D H D, so it runs before
+// wave_kernel with one thread per column (NTS threads per robot) and, for n <= 128, the column of H
+// generated once into registers instead of once per pass.  It writes a per-robot image (ScaleImg:
+// D, E, the scaled gradient q~, the raw gradient, the A entries the passes used, c, the warm-start
+// branch) that wave_kernel reads in place of its own setup.  H's columns come from the same closed
+// form as before (see gen_col), so every norm is binary64; only the order of the cost-scaling sum
+// over columns differs from the single-wave version (a different but equally exact summation).
+template <int N>
+struct ScaleImg {
+  static constexpr int n = ND * N, m = CD * N;
+  static constexpr int D = 0, E = D + n, Q = E + m, QN = Q + n, AP = QN + n, CS = AP + 2 * m, MODE = CS + 1,
+                       SIZE = MODE + 1;
+  static_assert(SIZE == scale_image_doubles(N), "scale image layout");
+};
+
+template <int N>
+struct ScaleCfg {
+  static constexpr int n = ND * N, m = CD * N;
+#ifndef MPCQP_SCALE_TPC
+#define MPCQP_SCALE_TPC 2
+#endif
+  static constexpr bool HREG = N <= 10;              // the thread's entries cached in registers
+  static constexpr int TPC = HREG ? MPCQP_SCALE_TPC : 1;  // threads per column (adjacent lanes)
+  static constexpr int BPT = (N + TPC - 1) / TPC;    // horizon blocks of the column per thread
+  static constexpr int NTS = ((TPC * n + 63) / 64) * 64;
+  static constexpr int NWS = NTS / 64;
+  static constexpr int WPE = NWS >= 2 ? NWS / 2 : 1;  // waves per SIMD for two robots per CU
+  static constexpr int RPT = (m + NTS - 1) / NTS;   // constraint rows per thread
+};
+
+template <int N>
+struct ScaleSmem {
+  using C = Cfg<N>;
+  alignas(16) double Bw[N][3][ND];
+  double rec[C::REC];
+  double D[C::n], Dt[C::n], q[C::n], qn[C::n], E[C::m];
+  double lam[N][ND];
+  double vec[2][16];
+  double Ap[2][C::m];
+  double red[2][16];
+};
+
+template <int NW>
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  if constexpr (NW == 1) {
+    return v;
+  } else {
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = red[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s += red[i];
+    return s;
+  }
+}
+template <int NW>
+__device__ __forceinline__ double block_max(double v, double* red) {
+  v = wave_max(v);
+  if constexpr (NW == 1) {
+    return v;
+  } else {
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = red[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s = fmax(s, red[i]);
+    return s;
+  }
+}
+
+// Column c of H = B'Q̄B + R in closed form (A_c is nilpotent on the 12 moving states, A_c^2 = 0,
+// so A^m = I + m Ac with Ac := dt A_c, and
+//   S_j = sum_{m=0}^{M_j} (A^m)' Q A^m = (M_j+1) Q + T1_j (Q Ac + Ac'Q) + T2_j Ac'Q Ac,
+//   M_j = N-1-j, T1 = M(M+1)/2, T2 = M(M+1)(2M+1)/6.  With y = B_k e_a (column c = 12k + a):
+//   block j <= k:  H_jk e_a = B_j' (A')^{k-j} S_k y = B_j' (g + (k-j) Ac'g),   g = S_k y
+//   block j >  k:  H_jk e_a = B_j' S_j A^{j-k} y   = B_j' S_j (y + (j-k) Ac y)
+// where only rows 6-11 of the 12-vector inside B_j' matter).  Blocks jb .. jb+NB-1 (< N) only;
+// sink(jj, b, ri, hv) receives entry ri = 12 j + b of block j = jb + jj, jj and b compile-time.
+template <int N, int NB, bool UNROLL, class Sink>
+__device__ __forceinline__ void gen_col(const ScaleSmem<N>& sm, const mpcqp_params& p, const Adisc& A, double dtm,
+                                        int c, int jb, Sink&& sink) {
+  const double dt = A.dt;
+  const int k = c / ND, a2 = c % ND;
+  double y[12], w[12];
+#pragma unroll
+  for (int s2 = 0; s2 < 12; ++s2) y[s2] = 0.0;
+  y[6] = sm.Bw[k][0][a2];
+  y[7] = sm.Bw[k][1][a2];
+  y[8] = sm.Bw[k][2][a2];
+  y[9 + a2 % 3] = dtm;
+  w[0] = A.ad0 * y[6] + A.ad1 * y[7];
+  w[1] = (-A.ad1) * y[6] + A.ad0 * y[7];
+  w[2] = dt * y[8];
+  w[3] = dt * y[9];
+  w[4] = dt * y[10];
+  w[5] = dt * y[11];
+#pragma unroll
+  for (int s2 = 6; s2 < 12; ++s2) w[s2] = 0.0;
+  double qy[12], qw[12];
+#pragma unroll
+  for (int s2 = 0; s2 < 12; ++s2) {
+    qy[s2] = 2 * p.q_weights[s2] * y[s2];
+    qw[s2] = 2 * p.q_weights[s2] * w[s2];
+  }
+  auto actv = [&](const double (&v)[12], double (&o)[6]) __attribute__((always_inline)) {
+    o[0] = A.ad0 * v[0] + (-A.ad1) * v[1];
+    o[1] = A.ad1 * v[0] + A.ad0 * v[1];
+    o[2] = dt * v[2];
+    o[3] = dt * v[3];
+    o[4] = dt * v[4];
+    o[5] = dt * v[5];
+  };
+  double u1[6], u2[6];
+  actv(qy, u1);
+  actv(qw, u2);
+  const double Mk = (double)(N - 1 - k);
+  const double T1k = Mk * (Mk + 1) / 2, T2k = Mk * (Mk + 1) * (2 * Mk + 1) / 6;
+  double g[12];
+#pragma unroll
+  for (int s2 = 0; s2 < 12; ++s2) {
+    const double ac = s2 >= 6 ? u1[s2 - 6] : 0.0, ac2 = s2 >= 6 ? u2[s2 - 6] : 0.0;
+    g[s2] = ((Mk + 1) * qy[s2] + T1k * (qw[s2] + ac)) + T2k * ac2;
+  }
+  double h[6];
+  actv(g, h);
+  auto block = [&](int jj) __attribute__((always_inline)) {
+    const int j = jb + jj;
+    if (j >= N) return;
+    const bool up = j <= k;
+    const double d = (double)(j - k);
+    const double Mj = (double)(N - 1 - j);
+    const double T1j = Mj * (Mj + 1) / 2, T2j = Mj * (Mj + 1) * (2 * Mj + 1) / 6;
+    const double cg = up ? 1.0 : 0.0, ch = up ? -d : 0.0;
+    const double cqy = up ? 0.0 : Mj + 1, cqw = up ? 0.0 : (Mj + 1) * d + T1j;
+    const double cu1 = up ? 0.0 : T1j, cu2 = up ? 0.0 : T1j * d + T2j;
+    double v[6];
+#pragma unroll
+    for (int s2 = 0; s2 < 6; ++s2)
+      v[s2] = ((((cg * g[6 + s2] + ch * h[s2]) + cqy * qy[6 + s2]) + cqw * qw[6 + s2]) + cu1 * u1[s2]) + cu2 * u2[s2];
+    const double* bw0 = sm.Bw[j][0];
+    const double* bw1 = sm.Bw[j][1];
+    const double* bw2 = sm.Bw[j][2];
+#pragma unroll
+    for (int b = 0; b < 12; ++b) {
+      double hv = ((bw0[b] * v[0] + bw1[b] * v[1]) + bw2[b] * v[2]) + dtm * v[3 + b % 3];
+      if (j == k && b == a2) hv += 2 * p.r_weights[b];
+      sink(jj, b, ND * j + b, hv);
+    }
+  };
+  if constexpr (UNROLL) {
+    sfor<0, NB>([&](auto JJ) __attribute__((always_inline)) { block(decltype(JJ)::value); });
+  } else {
+#pragma unroll 1
+    for (int jj = 0; jj < NB; ++jj) block(jj);
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kernel(const double* __restrict__ recs, int batch,
+                                                                 double* __restrict__ wstate,
+                                                                 double* __restrict__ img, mpcqp_params p) {
+  using C = Cfg<N>;
+  using SC = ScaleCfg<N>;
+  using WL = WarmLayout<N>;
+  using SI = ScaleImg<N>;
+  constexpr int n = C::n, m = C::m, NTS = SC::NTS;
+  __shared__ ScaleSmem<N> sm;
+  const int inst = blockIdx.x;
+  if (inst >= batch) return;
+  const int t = threadIdx.x;
+  {
+    const double* rg = recs + (size_t)inst * C::REC;
+    int bad = 0;
+    for (int e = t; e < C::REC; e += NTS) {
+      const double v = rg[e];
+      sm.rec[e] = v;
+      bad |= !isfinite(v);
+    }
+    if (__syncthreads_or(bad)) return;  // wave_kernel reports the non-finite record
+  }
+  const double* rec = sm.rec;
+  const double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS], mu = rec[MPCQP_REC_MU];
+  Adisc A;
+  {
+    const double yaw = rec[MPCQP_REC_EULER + 2];
+    A.ad0 = cos(yaw) * dt;
+    A.ad1 = sin(yaw) * dt;
+    A.dt = dt;
+  }
+  const double dtm = (1.0 / mass) * dt;
+  // B_d(k) rows 6-8 (calculate_B_mat_c, Utils.cpp:35-41), gradient adjoint (ConvexMpc.cpp:215-217)
+  {
+    double Iwinv[9];
+    iw_inverse(rec, Iwinv);
+    for (int e = t; e < N * 36; e += NTS) {
+      const int k = e / 36, rr = (e / 12) % 3, cc = e % 12;
+      const int lg = cc / 3, c3 = cc % 3;
+      const double* fp = rec + MPCQP_REC_FEET(N) + 12 * k + 3 * lg;
+      const double sk0 = c3 == 0 ? 0.0 : c3 == 1 ? -fp[2] : fp[1];
+      const double sk1 = c3 == 0 ? fp[2] : c3 == 1 ? 0.0 : -fp[0];
+      const double sk2 = c3 == 0 ? -fp[1] : c3 == 1 ? fp[0] : 0.0;
+      double s = 0.0;
+      s += sel3(rr, Iwinv[0], Iwinv[3], Iwinv[6]) * sk0;
+      s += sel3(rr, Iwinv[1], Iwinv[4], Iwinv[7]) * sk1;
+      s += sel3(rr, Iwinv[2], Iwinv[5], Iwinv[8]) * sk2;
+      sm.Bw[k][rr][cc] = s * dt;
+    }
+    // forward: a_i = A_d^{i+1} x0 (13 states), e_i = 2q (a_i - x_ref_i); backward: lambda_j = e_j + A' lambda_{j+1}
+    if (t < SD) sm.vec[0][t] = rec[MPCQP_REC_X0 + t];
+    __syncthreads();
+    for (int i = 0; i < N; ++i) {
+      if (t < SD) {
+        const double* pv = sm.vec[i & 1];
+        double s;
+        if (t == 0) s = (pv[0] + A.ad0 * pv[6]) + A.ad1 * pv[7];
+        else if (t == 1) s = (pv[1] + (-A.ad1) * pv[6]) + A.ad0 * pv[7];
+        else if (t == 2) s = pv[2] + dt * pv[8];
+        else if (t <= 5) s = pv[t] + dt * pv[t + 6];
+        else if (t == 11) s = pv[11] + dt * pv[12];
+        else s = pv[t];
+        sm.vec[(i + 1) & 1][t] = s;
+        if (t < ND) sm.lam[i][t] = 2 * p.q_weights[t] * (s - rec[MPCQP_REC_XREF + SD * i + t]);
+      }
+      __syncthreads();
+    }
+    for (int j = N - 2; j >= 0; --j) {
+      if (t < ND) sm.lam[j][t] = sm.lam[j][t] + A.atv(t, sm.lam[j + 1]);
+      __syncthreads();
+    }
+  }
+  // thread t: column j0 = t / 4, blocks jb .. jb+BPT-1 of it (the column's four threads are a quad)
+  constexpr int BPT = SC::BPT;
+  const int j0 = t / SC::TPC, jb = (t % SC::TPC) * BPT;
+  const bool lead = (t % SC::TPC) == 0;  // the lane that owns the column's per-column values
+  if (lead && j0 < n) {
+    const int k = j0 / ND, ii = j0 % ND;
+    const double* lm = sm.lam[k];
+    const double g = ((sm.Bw[k][0][ii] * lm[6] + sm.Bw[k][1][ii] * lm[7]) + sm.Bw[k][2][ii] * lm[8]) + dtm * lm[9 + ii % 3];
+    sm.q[j0] = g;
+    sm.qn[j0] = g;
+    sm.D[j0] = 1.0;
+  }
+  for (int r = t; r < m; r += NTS) {
+    sm.E[r] = 1.0;
+    const int a5 = r % 5;  // friction pyramid rows (ConvexMpc.cpp:46-58)
+    sm.Ap[0][r] = a5 < 4 ? 1.0 : 0.0;
+    sm.Ap[1][r] = a5 < 4 ? ((a5 & 1) ? -mu : mu) : 1.0;
+  }
+  __syncthreads();
+  double* const ws = wstate ? wstate + (size_t)inst * WL::SIZE : nullptr;
+  const bool had = ws && ws[WL::FLAG] != 0.0;
+  // max_i D_i |H_ij0| over the thread's blocks, then over the quad (every lane of it gets the norm)
+  double hc[SC::HREG ? 12 * BPT : 1];
+  auto colmax = [&](bool first) __attribute__((always_inline)) -> double {
+    double mx0 = 0.0, mx1 = 0.0;
+    if (j0 < n) {
+      if constexpr (SC::HREG) {
+        if (first)
+          gen_col<N, BPT, true>(sm, p, A, dtm, j0, jb, [&](int jj, int b, int, double hv) __attribute__((always_inline)) {
+            hc[12 * jj + b] = hv;
+          });
+#pragma unroll
+        for (int jj = 0; jj < BPT; ++jj) {
+          const int j = jb + jj;
+          if (j < N) {
+            const double* dj = sm.D + ND * j;
+#pragma unroll
+            for (int b = 0; b < 12; ++b) {
+              if (b & 1) mx1 = fmax(mx1, dj[b] * dabs(hc[12 * jj + b]));
+              else mx0 = fmax(mx0, dj[b] * dabs(hc[12 * jj + b]));
+            }
+          }
+        }
+      } else {
+        gen_col<N, BPT, false>(sm, p, A, dtm, j0, jb, [&](int, int b, int ri, double hv) __attribute__((always_inline)) {
+          if (b & 1) mx1 = fmax(mx1, sm.D[ri] * dabs(hv));
+          else mx0 = fmax(mx0, sm.D[ri] * dabs(hv));
+        });
+      }
+    }
+    double mx = fmax(mx0, mx1);
+    if constexpr (SC::TPC >= 2) mx = fmax(mx, dpp<0xB1>(mx));  // over the column's lanes
+    if constexpr (SC::TPC == 4) mx = fmax(mx, dpp<0x4E>(mx));
+    return mx;
+  };
+  // H's zero pattern (sparseView) of column j0's upper triangle vs the previous tick's: decides
+  // between osqp_update_P and OsqpEigen's re-init (oracle ws_update)
+  auto pattern = [&]() __attribute__((always_inline)) -> bool {
+    unsigned long long zm[WL::MW];
+#pragma unroll
+    for (int w = 0; w < WL::MW; ++w) zm[w] = 0ull;
+    auto put = [&](int, int, int ri, double hv) __attribute__((always_inline)) {
+      const unsigned long long bit = (hv == 0.0 && ri <= j0) ? (1ull << (ri & 63)) : 0ull;
+#pragma unroll
+      for (int w = 0; w < WL::MW; ++w) zm[w] |= (ri >> 6) == w ? bit : 0ull;
+    };
+    if (j0 < n) {
+      if constexpr (SC::HREG) {
+#pragma unroll
+        for (int jj = 0; jj < BPT; ++jj)
+#pragma unroll
+          for (int b = 0; b < 12; ++b)
+            if (jb + jj < N) put(jj, b, ND * (jb + jj) + b, hc[12 * jj + b]);
+      } else {
+        gen_col<N, BPT, false>(sm, p, A, dtm, j0, jb, put);
+      }
+    }
+    bool diff = false;
+#pragma unroll
+    for (int w = 0; w < WL::MW; ++w) {  // OR over the column's lanes
+      unsigned lo = (unsigned)zm[w], hi = (unsigned)(zm[w] >> 32);
+      if constexpr (SC::TPC >= 2) {
+        lo |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false);
+        hi |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false);
+      }
+      if constexpr (SC::TPC == 4) {
+        lo |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)lo, 0x4E, 0xF, 0xF, false);
+        hi |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)hi, 0x4E, 0xF, 0xF, false);
+      }
+      zm[w] = ((unsigned long long)hi << 32) | lo;
+    }
+    if (lead && j0 < n) {
+      double* slot = ws + WL::MASK + WL::MW * j0;
+#pragma unroll
+      for (int w = 0; w < WL::MW; ++w) {
+        diff |= __double_as_longlong(slot[w]) != (long long)zm[w];
+        slot[w] = __longlong_as_double((long long)zm[w]);
+      }
+    }
+    return diff;
+  };
+  auto acol = [&](int j) __attribute__((always_inline)) {
+    const int f = j / 3, aa = j % 3;
+    const double* e = sm.E + 5 * f;
+    const double* a0 = sm.Ap[0] + 5 * f;
+    const double* a1 = sm.Ap[1] + 5 * f;
+    double mx;
+    if (aa == 0) mx = dmax(e[0] * dabs(a0[0]), e[1] * dabs(a0[1]));
+    else if (aa == 1) mx = dmax(e[2] * dabs(a0[2]), e[3] * dabs(a0[3]));
+    else
+      mx = dmax(dmax(dmax(dmax(dabs(a1[0]) * e[0], dabs(a1[1]) * e[1]), dabs(a1[2]) * e[2]), dabs(a1[3]) * e[3]),
+                e[4] * dabs(a1[4]));
+    return mx * sm.D[j];
+  };
+  auto arow = [&](int r) __attribute__((always_inline)) {
+    const int f = r / 5, k5 = r % 5;
+    const double e = sm.E[r];
+    const double* d = sm.D + 3 * f;
+    if (k5 == 4) return (e * dabs(sm.Ap[1][r])) * d[2];
+    return dmax((e * dabs(sm.Ap[0][r])) * d[k5 >> 1], (dabs(sm.Ap[1][r]) * e) * d[2]);
+  };
+  double c_s = 1.0, cm = 0.0;
+  // First column pass (D = 1): the raw norms, and H's zero pattern (warm start only): same pattern
+  // -> osqp_update_P (unscale with the old scaling, rescale with the previous A and q, keep iterates
+  // and rho); a changed pattern or mu -> re-init (fresh scaling and rho, the previous unscaled x, y)
+  bool pattern_changed = false;
+  if (p.scaling > 0 || ws) {
+    cm = colmax(true);
+    if (ws) pattern_changed = __syncthreads_or(pattern()) != 0;
+  }
+  // A is set once per solver init (A1RobotControl.cpp:526-530); a changed mu re-initializes
+  const bool mu_changed = had && ws[WL::MU] != mu;
+  const int mode = !had ? 0 : ((pattern_changed || mu_changed) ? 2 : 1);  // 0 cold, 1 update_P, 2 re-init
+  if (mode == 1) {
+    // unscale_data with the previous scaling: q = D^-1 (c^-1 q~), A = (E^-1 A~) D^-1
+    const double cinv_o = 1. / ws[WL::C];
+    if (lead && j0 < n) sm.q[j0] = (1. / ws[WL::D + j0]) * (cinv_o * ws[WL::QT + j0]);
+    for (int r = t; r < m; r += NTS) {
+      const int f = r / 5, k5 = r % 5;
+      const double ei = 1. / ws[WL::E + r];
+      const double d2 = 1. / ws[WL::D + 3 * f + 2];
+      sm.Ap[0][r] = k5 < 4 ? (ws[WL::AK + r] * ei) * (1. / ws[WL::D + 3 * f + (k5 >> 1)]) : 0.0;
+      sm.Ap[1][r] = (ws[WL::AK + m + r] * ei) * d2;
+    }
+    __syncthreads();
+  }
+  for (int pass = 0; pass < p.scaling; ++pass) {
+    if (lead && j0 < n) {
+      const double pc = (c_s * sm.D[j0]) * cm;
+      sm.Dt[j0] = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j0))));
+    }
+    double et[SC::RPT];
+#pragma unroll
+    for (int rr = 0; rr < SC::RPT; ++rr) {
+      const int r = t + NTS * rr;
+      et[rr] = r < m ? 1.0 / sqrt(limit_scaling(arow(r))) : 1.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < SC::RPT; ++rr) {
+      const int r = t + NTS * rr;
+      if (r < m) sm.E[r] *= et[rr];
+    }
+    if (lead && j0 < n) {
+      sm.q[j0] = sm.Dt[j0] * sm.q[j0];
+      sm.D[j0] = sm.D[j0] * sm.Dt[j0];
+    }
+    __syncthreads();
+    cm = colmax(false);  // column norms of the D-scaled P (cost normalization)
+    double sv = 0.0, qv = 0.0;
+    if (lead && j0 < n) {
+      sv = (c_s * sm.D[j0]) * cm;
+      qv = dabs(sm.q[j0]);
+    }
+    sv = block_sum<SC::NWS>(sv, sm.red[0]);
+    qv = block_max<SC::NWS>(qv, sm.red[1]);
+    double c_temp = sv / n;
+    const double inf_norm_q = limit_scaling(qv);
+    c_temp = dmax(c_temp, inf_norm_q);
+    c_temp = limit_scaling(c_temp);
+    c_temp = 1. / c_temp;
+    if (lead && j0 < n) sm.q[j0] *= c_temp;
+    c_s *= c_temp;
+    __syncthreads();
+  }
+  double* out = img + (size_t)inst * SI::SIZE;
+  if (lead && j0 < n) {
+    out[SI::D + j0] = sm.D[j0];
+    out[SI::Q + j0] = sm.q[j0];
+    out[SI::QN + j0] = sm.qn[j0];
+  }
+  for (int r = t; r < m; r += NTS) {
+    out[SI::E + r] = sm.E[r];
+    out[SI::AP + r] = sm.Ap[0][r];
+    out[SI::AP + m + r] = sm.Ap[1][r];
+  }
+  if (t == 0) {
+    out[SI::CS] = c_s;
+    out[SI::MODE] = (double)mode;
+  }
+}
+
 // Phase timing (debug builds with -DMPCQP_PHASE_TIMING): lane 0 of each traced robot appends
 // {phase id, s_memtime, s_memrealtime (100 MHz), 0} to the trace buffer instead of check records.
 #ifdef MPCQP_PHASE_TIMING
@@ -505,7 +939,8 @@ template <int N>
 __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ recs, int batch,
                                                      mpcqp_result* __restrict__ results,
                                                      double* __restrict__ solution, double* __restrict__ trace,
-                                                     int trace_cap, double* __restrict__ wstate, mpcqp_params p) {
+                                                     int trace_cap, double* __restrict__ wstate,
+                                                     const double* __restrict__ img, mpcqp_params p) {
   using C = Cfg<N>;
   using WL = WarmLayout<N>;
   constexpr int n = C::n, m = C::m, R = C::R;
@@ -581,259 +1016,29 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       s += sel3(rr, Iwinv[2], Iwinv[5], Iwinv[8]) * sk2;
       sm.Bw[k][rr][cc] = s * dt;
     }
-    // forward: a_i = A_d^{i+1} x0 (13 states), e_i = 2q (a_i - x_ref_i) (ConvexMpc.cpp:215-217)
-    if (t < SD) HS.vec[0][t] = rec[MPCQP_REC_X0 + t];
-    wave_sync();
-    for (int i = 0; i < N; ++i) {
-      if (t < SD) {
-        const double* pv = HS.vec[i & 1];
-        double s;
-        if (t == 0) s = (pv[0] + A.ad0 * pv[6]) + A.ad1 * pv[7];
-        else if (t == 1) s = (pv[1] + (-A.ad1) * pv[6]) + A.ad0 * pv[7];
-        else if (t == 2) s = pv[2] + dt * pv[8];
-        else if (t <= 5) s = pv[t] + dt * pv[t + 6];
-        else if (t == 11) s = pv[11] + dt * pv[12];
-        else s = pv[t];
-        HS.vec[(i + 1) & 1][t] = s;
-        if (t < ND) HS.lam[i][t] = 2 * p.q_weights[t] * (s - rec[MPCQP_REC_XREF + SD * i + t]);
-      }
-      wave_sync();
-    }
-    // backward: lambda_j = e_j + A' lambda_{j+1}
-    for (int j = N - 2; j >= 0; --j) {
-      if (t < ND) HS.lam[j][t] = HS.lam[j][t] + A.atv(t, HS.lam[j + 1]);
-      wave_sync();
-    }
   }
   WV_MARK(2);
 
   WV_MARK(3);
 
-  // ---- 3. OSQP scale_data (scaling.c) with the scaling deferred: P~ = c D H D is never formed -------
-  // Column inf-norms of P~ are (c D_j) max_i D_i |H_ij| (H symmetric).  H is never stored either:
-  // every pass regenerates the lane's columns c = t, t + 64 of H = B'Q̄B + R in binary64.  A_c is
-  // nilpotent on the 12 moving states (A_c^2 = 0), so A^m = I + m Ac (Ac := dt A_c) and
-  //   S_j = sum_{m=0}^{M_j} (A^m)' Q A^m = (M_j+1) Q + T1_j (Q Ac + Ac'Q) + T2_j Ac'Q Ac,
-  //   M_j = N-1-j, T1 = M(M+1)/2, T2 = M(M+1)(2M+1)/6.  With y = B_k e_a (column c = 12k + a):
-  //   block j <= k:  H_jk e_a = B_j' (A')^{k-j} S_k y = B_j' (g + (k-j) Ac'g),   g = S_k y
-  //   block j >  k:  H_jk e_a = B_j' S_j A^{j-k} y   = B_j' S_j (y + (j-k) Ac y)
-  // and only rows 6-11 of the 12-vector inside B_j' matter.  A~ = E A D entries are E_r |A_rj| D_j
-  // (A: ConvexMpc.cpp:46-58, entries 1 and +-mu).
+  // ---- 3. OSQP scale_data: the image scale_kernel wrote (D, E, q~, raw q, A entries, c, branch) ----
+  using SI = ScaleImg<N>;
+  const double* im = img + (size_t)inst * SI::SIZE;
   for (int j = t; j < n; j += NT) {
-    const int k = j / ND, ii = j % ND;
-    const double* lm = HS.lam[k];
-    const double g = ((sm.Bw[k][0][ii] * lm[6] + sm.Bw[k][1][ii] * lm[7]) + sm.Bw[k][2][ii] * lm[8]) + dtm * lm[9 + ii % 3];
-    HS.q[j] = g;
-    HS.qn[j] = g;
-    HS.D[j] = 1.0;
+    HS.D[j] = im[SI::D + j];
+    HS.q[j] = im[SI::Q + j];
+    HS.qn[j] = im[SI::QN + j];
   }
   for (int r = t; r < m; r += NT) {
-    HS.E[r] = 1.0;
-    const int a5 = r % 5;  // friction pyramid rows (ConvexMpc.cpp:46-58)
-    HS.Ap[0][r] = a5 < 4 ? 1.0 : 0.0;
-    HS.Ap[1][r] = a5 < 4 ? ((a5 & 1) ? -mu : mu) : 1.0;
+    HS.E[r] = im[SI::E + r];
+    HS.Ap[0][r] = im[SI::AP + r];
+    HS.Ap[1][r] = im[SI::AP + m + r];
   }
-  wave_sync();
+  const double c_s = im[SI::CS];
+  const int mode = (int)im[SI::MODE];  // 0 cold, 1 osqp_update_P, 2 OsqpEigen re-init
   // Warm start (A1RobotControl.h:67 member solver, :522-538): the slot of the previous tick.
   double* const ws = wstate ? wstate + (size_t)inst * WL::SIZE : nullptr;
-  const bool had = ws && ws[WL::FLAG] != 0.0;
-  auto colmax1 = [&](int c, unsigned long long (&zm)[WL::MW], auto with_mask) __attribute__((always_inline)) -> double {
-    // max_i D_i |H_ic|; zm collects the exact zeros of column c's upper triangle (sparseView)
-    const int k = c / ND, a2 = c % ND;
-    double y[12], w[12];
-#pragma unroll
-    for (int s2 = 0; s2 < 12; ++s2) y[s2] = 0.0;
-    y[6] = sm.Bw[k][0][a2];
-    y[7] = sm.Bw[k][1][a2];
-    y[8] = sm.Bw[k][2][a2];
-    y[9 + a2 % 3] = dtm;
-    w[0] = A.ad0 * y[6] + A.ad1 * y[7];
-    w[1] = (-A.ad1) * y[6] + A.ad0 * y[7];
-    w[2] = dt * y[8];
-    w[3] = dt * y[9];
-    w[4] = dt * y[10];
-    w[5] = dt * y[11];
-#pragma unroll
-    for (int s2 = 6; s2 < 12; ++s2) w[s2] = 0.0;
-    double qy[12], qw[12];
-#pragma unroll
-    for (int s2 = 0; s2 < 12; ++s2) {
-      qy[s2] = 2 * p.q_weights[s2] * y[s2];
-      qw[s2] = 2 * p.q_weights[s2] * w[s2];
-    }
-    auto actv = [&](const double (&v)[12], double (&o)[6]) __attribute__((always_inline)) {
-      o[0] = A.ad0 * v[0] + (-A.ad1) * v[1];
-      o[1] = A.ad1 * v[0] + A.ad0 * v[1];
-      o[2] = dt * v[2];
-      o[3] = dt * v[3];
-      o[4] = dt * v[4];
-      o[5] = dt * v[5];
-    };
-    double u1[6], u2[6];
-    actv(qy, u1);
-    actv(qw, u2);
-    const double Mk = (double)(N - 1 - k);
-    const double T1k = Mk * (Mk + 1) / 2, T2k = Mk * (Mk + 1) * (2 * Mk + 1) / 6;
-    double g[12];
-#pragma unroll
-    for (int s2 = 0; s2 < 12; ++s2) {
-      const double ac = s2 >= 6 ? u1[s2 - 6] : 0.0, ac2 = s2 >= 6 ? u2[s2 - 6] : 0.0;
-      g[s2] = ((Mk + 1) * qy[s2] + T1k * (qw[s2] + ac)) + T2k * ac2;
-    }
-    double h[6];
-    actv(g, h);
-    double mx0 = 0.0, mx1 = 0.0;
-#pragma unroll 1
-    for (int j = 0; j < N; ++j) {
-      const bool up = j <= k;
-      const double d = (double)(j - k);
-      const double Mj = (double)(N - 1 - j);
-      const double T1j = Mj * (Mj + 1) / 2, T2j = Mj * (Mj + 1) * (2 * Mj + 1) / 6;
-      const double cg = up ? 1.0 : 0.0, ch = up ? -d : 0.0;
-      const double cqy = up ? 0.0 : Mj + 1, cqw = up ? 0.0 : (Mj + 1) * d + T1j;
-      const double cu1 = up ? 0.0 : T1j, cu2 = up ? 0.0 : T1j * d + T2j;
-      double v[6];
-#pragma unroll
-      for (int s2 = 0; s2 < 6; ++s2)
-        v[s2] = ((((cg * g[6 + s2] + ch * h[s2]) + cqy * qy[6 + s2]) + cqw * qw[6 + s2]) + cu1 * u1[s2]) + cu2 * u2[s2];
-      const double* bw0 = sm.Bw[j][0];
-      const double* bw1 = sm.Bw[j][1];
-      const double* bw2 = sm.Bw[j][2];
-      const double* dj = HS.D + ND * j;
-#pragma unroll
-      for (int b = 0; b < 12; ++b) {
-        double hv = ((bw0[b] * v[0] + bw1[b] * v[1]) + bw2[b] * v[2]) + dtm * v[3 + b % 3];
-        if (j == k && b == a2) hv += 2 * p.r_weights[b];
-        if (b & 1) mx1 = fmax(mx1, dj[b] * dabs(hv));
-        else mx0 = fmax(mx0, dj[b] * dabs(hv));
-        if constexpr (decltype(with_mask)::value) {
-          const int ri = ND * j + b;  // row index; its bit in word ri >> 6
-          const unsigned long long bit = (hv == 0.0 && ri <= c) ? (1ull << (ri & 63)) : 0ull;
-#pragma unroll
-          for (int w = 0; w < WL::MW; ++w) zm[w] |= (ri >> 6) == w ? bit : 0ull;
-        }
-      }
-    }
-    return fmax(mx0, mx1);
-  };
-  constexpr int NC = (C::n + NT - 1) / NT;  // columns per lane: t, t + 64, ...
-  auto colmax = [&](double (&cm)[NC], bool masks) __attribute__((always_inline)) {
-    bool diff = false;
-#pragma unroll
-    for (int h = 0; h < NC; ++h) {
-      const int c = t + NT * h;
-      unsigned long long zm[WL::MW];
-#pragma unroll
-      for (int w = 0; w < WL::MW; ++w) zm[w] = 0ull;
-      if (masks) {
-        cm[h] = c < n ? colmax1(c, zm, IC<1>{}) : 0.0;
-      } else {
-        cm[h] = c < n ? colmax1(c, zm, IC<0>{}) : 0.0;
-      }
-      if (masks && c < n) {  // compare with and replace the previous tick's pattern
-        double* slot = ws + WL::MASK + WL::MW * c;
-#pragma unroll
-        for (int w = 0; w < WL::MW; ++w) {
-          diff |= __double_as_longlong(slot[w]) != (long long)zm[w];
-          slot[w] = __longlong_as_double((long long)zm[w]);
-        }
-      }
-    }
-    return __ballot(diff) != 0;
-  };
-  // column norm of A~ for variable j / row norm of A~ for row r (A entries from HS.Ap)
-  auto acol = [&](int j) __attribute__((always_inline)) {
-    const int f = j / 3, aa = j % 3;
-    const double* e = HS.E + 5 * f;
-    const double* a0 = HS.Ap[0] + 5 * f;
-    const double* a1 = HS.Ap[1] + 5 * f;
-    double mx;
-    if (aa == 0) mx = dmax(e[0] * dabs(a0[0]), e[1] * dabs(a0[1]));
-    else if (aa == 1) mx = dmax(e[2] * dabs(a0[2]), e[3] * dabs(a0[3]));
-    else
-      mx = dmax(dmax(dmax(dmax(dabs(a1[0]) * e[0], dabs(a1[1]) * e[1]), dabs(a1[2]) * e[2]), dabs(a1[3]) * e[3]),
-                e[4] * dabs(a1[4]));
-    return mx * HS.D[j];
-  };
-  auto arow = [&](int r) __attribute__((always_inline)) {
-    const int f = r / 5, k5 = r % 5;
-    const double e = HS.E[r];
-    const double* d = HS.D + 3 * f;
-    if (k5 == 4) return (e * dabs(HS.Ap[1][r])) * d[2];
-    return dmax((e * dabs(HS.Ap[0][r])) * d[k5 >> 1], (dabs(HS.Ap[1][r]) * e) * d[2]);
-  };
-  double c_s = 1.0, cm[NC];
-#pragma unroll
-  for (int h = 0; h < NC; ++h) cm[h] = 0.0;
-  // First column pass (D = 1): the raw norms, and H's zero pattern, which decides the warm-start
-  // branch of OsqpEigen 0.6.3 updateHessianMatrix: same pattern -> osqp_update_P (unscale with the
-  // old scaling, rescale with the previous A and q, keep iterates and rho); a changed pattern ->
-  // re-init (fresh scaling and rho) with the previous unscaled x, y restored (oracle ws_update).
-  const bool pattern_changed = (p.scaling > 0 || ws) ? colmax(cm, ws != nullptr) : false;
-  // A is set once per solver init (A1RobotControl.cpp:526-530); a robot whose mu changed gets a
-  // re-init with the new friction cone rather than update_P on the old one (oracle ws_update).
-  const bool mu_changed = had && ws[WL::MU] != mu;
-  const int mode = !had ? 0 : ((pattern_changed || mu_changed) ? 2 : 1);  // 0 cold, 1 update_P, 2 re-init
-  if (mode == 1) {
-    // unscale_data with the previous scaling: q = D^-1 (c^-1 q~), A = (E^-1 A~) D^-1
-    const double cinv_o = 1. / ws[WL::C];
-    for (int j = t; j < n; j += NT) HS.q[j] = (1. / ws[WL::D + j]) * (cinv_o * ws[WL::QT + j]);
-    for (int r = t; r < m; r += NT) {
-      const int f = r / 5, k5 = r % 5;
-      const double ei = 1. / ws[WL::E + r];
-      const double d2 = 1. / ws[WL::D + 3 * f + 2];
-      HS.Ap[0][r] = k5 < 4 ? (ws[WL::AK + r] * ei) * (1. / ws[WL::D + 3 * f + (k5 >> 1)]) : 0.0;
-      HS.Ap[1][r] = (ws[WL::AK + m + r] * ei) * d2;
-    }
-    wave_sync();
-  }
-  for (int pass = 0; pass < p.scaling; ++pass) {
-#pragma unroll
-    for (int h = 0; h < NC; ++h) {
-      const int j = t + NT * h;
-      if (j < n) {
-        const double pc = (c_s * HS.D[j]) * cm[h];
-        HS.Dt[j] = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j))));
-      }
-    }
-    double et[(C::m + NT - 1) / NT];
-#pragma unroll
-    for (int rr = 0; rr < (C::m + NT - 1) / NT; ++rr) {
-      const int r = t + NT * rr;
-      et[rr] = r < m ? 1.0 / sqrt(limit_scaling(arow(r))) : 1.0;
-    }
-    wave_sync();
-#pragma unroll
-    for (int rr = 0; rr < (C::m + NT - 1) / NT; ++rr) {
-      const int r = t + NT * rr;
-      if (r < m) HS.E[r] *= et[rr];
-    }
-    for (int j = t; j < n; j += NT) {
-      HS.q[j] = HS.Dt[j] * HS.q[j];
-      HS.D[j] = HS.D[j] * HS.Dt[j];
-    }
-    wave_sync();
-    colmax(cm, false);  // column norms of the D-scaled P (cost normalization)
-    double sv = 0.0, qv = 0.0;
-#pragma unroll
-    for (int h = 0; h < NC; ++h) {
-      const int j = t + NT * h;
-      if (j < n) {
-        sv += (c_s * HS.D[j]) * cm[h];
-        qv = fmax(qv, dabs(HS.q[j]));
-      }
-    }
-    sv = wave_sum(sv);
-    qv = wave_max(qv);
-    double c_temp = sv / n;
-    const double inf_norm_q = limit_scaling(qv);
-    c_temp = dmax(c_temp, inf_norm_q);
-    c_temp = limit_scaling(c_temp);
-    c_temp = 1. / c_temp;
-    for (int j = t; j < n; j += NT) HS.q[j] *= c_temp;
-    c_s *= c_temp;
-    wave_sync();
-  }
+  wave_sync();
   const double cost_c = c_s, cinv = 1. / c_s;
   WV_MARK(4);
 
@@ -1416,8 +1621,12 @@ __global__ void wave_selftest_kernel(double* out) {
 
 template <int N>
 static hipError_t launch_wave(const LaunchArgs& a) {
+  hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
+                     a.recs, a.batch, a.wstate, a.work, a.p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((wv::wave_kernel<N>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs, a.batch,
-                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.p);
+                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p);
   return hipGetLastError();
 }
 template <int N>
