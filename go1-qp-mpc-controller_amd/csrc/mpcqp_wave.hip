@@ -166,6 +166,21 @@ __device__ __forceinline__ void mv_rounds(const double (&x)[R], const double (&c
     for (int r = 0; r < R; ++r) y[r] = mv12(x[r], c[r]);
   }
 }
+// init + sum_c M[c] x_c: the chains' "- a_k" / "+ h_k" folded into the first accumulator
+__device__ __forceinline__ double mv12a(double x, const double (&c)[12], double init) {
+  double a0 = init, a1 = 0.0, a2 = 0.0;
+  asm("s_nop 4\n\t"
+      WV_FM("%[a1]", "%[c1]", 1) WV_FM("%[a2]", "%[c2]", 2) WV_FM("%[a0]", "%[c0]", 0)
+      WV_FM("%[a1]", "%[c4]", 5) WV_FM("%[a2]", "%[c5]", 6) WV_FM("%[a0]", "%[c3]", 4)
+      WV_FM("%[a1]", "%[c7]", 9) WV_FM("%[a2]", "%[c8]", 10) WV_FM("%[a0]", "%[c6]", 8)
+      WV_FM("%[a1]", "%[c10]", 13) WV_FM("%[a2]", "%[c11]", 14) WV_FM("%[a0]", "%[c9]", 12)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
+        [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]),
+        [c11] "v"(c[11]));
+  return (a1 + a2) + a0;
+}
+
 #undef WV_FM
 
 // quad_perm DPP of a double
@@ -191,6 +206,35 @@ __device__ __forceinline__ double rmove(double v) {
     const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
     return FROM < TO ? __hiloint2double((int)h2[0], (int)l2[0]) : __hiloint2double((int)h2[1], (int)l2[1]);
   }
+}
+
+// rmove without register copies: one permlane swap per dword (the source's other rows are
+// clobbered, the result's other rows are undefined).
+template <int FROM, int TO>
+__device__ __forceinline__ double rmove2(double v) {
+  static_assert((FROM ^ TO) == 1 || (FROM ^ TO) == 2, "rows must differ in one bit");
+  unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v), ol, oh;
+  if constexpr ((FROM ^ TO) == 1) {
+    if constexpr (FROM < TO)  // vdst.odd <- src.even
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3"
+                   : "=&v"(ol), "=&v"(oh), "+v"(lo), "+v"(hi));
+    else  // src.even <- vdst.odd
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %2, %0\n\tv_permlane16_swap_b32 %3, %1"
+                   : "=&v"(ol), "=&v"(oh), "+v"(lo), "+v"(hi));
+  } else {
+    if constexpr (FROM < TO)  // vdst rows 2-3 <- src rows 0-1
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %2\n\tv_permlane32_swap_b32 %1, %3"
+                   : "=&v"(ol), "=&v"(oh), "+v"(lo), "+v"(hi));
+    else  // src rows 0-1 <- vdst rows 2-3
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %2, %0\n\tv_permlane32_swap_b32 %3, %1"
+                   : "=&v"(ol), "=&v"(oh), "+v"(lo), "+v"(hi));
+  }
+  return __hiloint2double((int)oh, (int)ol);
+}
+// sum of a lane's value over the four quads of its DPP row (component a of every leg)
+__device__ __forceinline__ double legsum(double v) {
+  v = v + dpp<0x128>(v);  // row_ror:8
+  return v + dpp<0x124>(v);  // row_ror:4
 }
 
 template <int V>
@@ -1209,7 +1253,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     const bool tm_it = iter == 60;
     if (tm_it) WV_MARK(40);
     {
-      double W[R], AKw[R], SMv[R], G[R], Hh[R], XS[R], c[R][12];
+      // LDS operands are loaded one phase ahead of their use; sched_barrier keeps the scheduler from
+      // sinking a prefetch back down to its consumer (counted lgkmcnt waits then cover only it).
+      double W[R], AKw[R], SMv[R], G[R], Hh[R], XS[R], tt[R];
+      double cA[R][12], cB[R][12], cw[R][3];
       int kc[R], kk[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -1219,65 +1266,79 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         kc[r] = min(4 * r + ig, N - 1);
         kk[r] = max(kc[r] - 1, 0);  // slot of K_k (k >= 1)
       }
-      // a_k = K_k' w_k (k >= 1)
+      double cn[12];
 #pragma unroll
-      for (int r = 0; r < R; ++r) ld12s(c[r], &F.K[kk[r]][idx]);
-      mv_rounds<R>(W, c, AKw);
+      for (int r = 0; r < R; ++r) ld12s(cA[r], &F.K[kk[r]][idx]);
+      if constexpr (N >= 3) ld12s(cn, &F.Acl[N - 3][idx]);
+      __builtin_amdgcn_sched_barrier(0);
+      // a_k = K_k' w_k (k >= 1)
+      mv_rounds<R>(W, cA, AKw);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {  // for g_k: G_k^-1 rows and B_k' columns
+        ld12(cB[r], &F.Gi[kc[r]][12 * idx]);
+        cw[r][0] = sm.Bw[kc[r]][0][idx];
+        cw[r][1] = sm.Bw[kc[r]][1][idx];
+        cw[r][2] = sm.Bw[kc[r]][2][idx];
+      }
+      __builtin_amdgcn_sched_barrier(0);
       if (tm_it) WV_MARK(41);
       {  // backward chain: s_{N-1} = -a_{N-1}; s_k = Acl_k' s_{k+1} - a_k; SMv (row of k) = s_{k+1}
         double cur = -AKw[(N - 1) >> 2];
-        double cn[12];
-        if constexpr (N >= 3) ld12s(cn, &F.Acl[N - 3][idx]);
         sfor<0, N - 1>([&](auto J) {
           constexpr int k = N - 2 - decltype(J)::value;
-          const double mvv = rmove<row_of(k + 1), row_of(k)>(cur);
+          const double mvv = rmove2<row_of(k + 1), row_of(k)>(cur);
           SMv[k >> 2] = (q == row_of(k)) ? mvv : SMv[k >> 2];
           if constexpr (k >= 1) {
             double cc[12];
 #pragma unroll
             for (int e = 0; e < 12; ++e) cc[e] = cn[e];
-            if constexpr (k >= 2) ld12s(cn, &F.Acl[k - 2][idx]);  // prefetch the next step's column
-            cur = mv12(mvv, cc) - AKw[k >> 2];
+            if constexpr (k >= 2) ld12s(cn, &F.Acl[k - 2][idx]);  // the next step's column
+            __builtin_amdgcn_sched_barrier(0);
+            cur = mv12a(mvv, cc, -AKw[k >> 2]);
           }
         });
       }
       if (tm_it) WV_MARK(42);
       // g_k = G_k^-1 (w_k + B_k' s_{k+1})
-      {
-        double tt[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const double c6[6] = {sm.Bw[kc[r]][0][idx], sm.Bw[kc[r]][1][idx], sm.Bw[kc[r]][2][idx],
-                                a == 0 ? dtm : 0.0, a == 1 ? dtm : 0.0, a == 2 ? dtm : 0.0};
-          tt[r] = W[r] + mv6(SMv[r], c6);
-          ld12(c[r], &F.Gi[kc[r]][12 * idx]);
-        }
-        mv_rounds<R>(tt, c, G);
-      }
-      // h_k = B_k g_k (rows 6-8: B_w, rows 9-11: dt/m on the matching force component)
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        ld12(c[r], &sm.Bw[kc[r]][av ? a : 2][0]);
-#pragma unroll
-        for (int e = 0; e < 12; ++e)
-          c[r][e] = (leg == 2 && av) ? c[r][e] : ((leg == 3 && av && e % 3 == a) ? dtm : 0.0);
+        const double c6[6] = {cw[r][0], cw[r][1], cw[r][2], a == 0 ? dtm : 0.0, a == 1 ? dtm : 0.0,
+                              a == 2 ? dtm : 0.0};
+        tt[r] = W[r] + mv6(SMv[r], c6);
       }
-      mv_rounds<R>(G, c, Hh);
+#pragma unroll
+      for (int r = 0; r < R; ++r) ld12(cA[r], &sm.Bw[kc[r]][av ? a : 2][0]);  // for h_k
+      __builtin_amdgcn_sched_barrier(0);
+      mv_rounds<R>(tt, cB, G);
+      // h_k = B_k g_k: rows 6-8 (leg-2 lanes) B_w g, rows 9-11 (leg-3 lanes) dt/m times the sum of
+      // the legs' matching force component, rows 0-5 zero
+      if constexpr (N >= 3) ld12(cn, &F.Acl[0][12 * idx]);
+#pragma unroll
+      for (int r = 0; r < R; ++r) ld12(cB[r], &F.K[kk[r]][12 * idx]);  // for u_k
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        double hb[R];
+        mv_rounds<R>(G, cA, hb);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const double ls = dtm * legsum(G[r]);
+          Hh[r] = leg == 2 ? hb[r] : (leg == 3 ? ls : 0.0);
+        }
+      }
       if (tm_it) WV_MARK(43);
       {  // forward chain: x_1 = h_0; x_{k+1} = Acl_k x_k + h_k; XS (row of k) = x_k
         double cur = Hh[0];
-        double cn[12];
-        if constexpr (N >= 3) ld12(cn, &F.Acl[0][12 * idx]);
         sfor<1, N>([&](auto K) {
           constexpr int k = decltype(K)::value;
-          const double mvv = rmove<row_of(k - 1), row_of(k)>(cur);
+          const double mvv = rmove2<row_of(k - 1), row_of(k)>(cur);
           XS[k >> 2] = (q == row_of(k)) ? mvv : XS[k >> 2];
           if constexpr (k <= N - 2) {
             double cc[12];
 #pragma unroll
             for (int e = 0; e < 12; ++e) cc[e] = cn[e];
-            if constexpr (k + 1 <= N - 2) ld12(cn, &F.Acl[k][12 * idx]);  // prefetch
-            cur = mv12(mvv, cc) + Hh[k >> 2];
+            if constexpr (k + 1 <= N - 2) ld12(cn, &F.Acl[k][12 * idx]);  // the next step's row
+            __builtin_amdgcn_sched_barrier(0);
+            cur = mv12a(mvv, cc, Hh[k >> 2]);
           }
         });
       }
@@ -1285,9 +1346,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       // u_k = g_k - K_k x_k (x_0 = 0)
       {
         double kx[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) ld12(c[r], &F.K[kk[r]][12 * idx]);
-        mv_rounds<R>(XS, c, kx);
+        mv_rounds<R>(XS, cB, kx);
 #pragma unroll
         for (int r = 0; r < R; ++r) U[r] = G[r] - kx[r];
       }
