@@ -52,10 +52,11 @@ def load_traffic(config_key, kernel):
             e = json.load(f).get(config_key, {})
     except (OSError, ValueError):
         return None
-    short = kernel.split("::")[-1].split("<")[0]  # e.g. wave_kernel
-    tmpl = kernel[kernel.find("<"):] if "<" in kernel else ""
-    if short not in e.get("kernel", "") or tmpl not in e.get("kernel", ""):
-        return None
+    for part in kernel.split(" + "):  # every kernel of the solve must be in the measured set
+        short = part.split("::")[-1].split("<")[0]  # e.g. wave_kernel
+        tmpl = part[part.find("<"):part.find(">") + 1] if "<" in part else ""
+        if short + tmpl not in e.get("kernel", "").replace(" ", ""):
+            return None
     return e.get("hbm_bytes_per_launch")
 
 
@@ -179,7 +180,7 @@ def main():
         key = f"N{N}_B{B}_{args.gait}{'_mu' if args.mixed_mu else ''}"
         eff = path or 3
         kernel_name = {1: f"mpcqp::solve_kernel<{N}>", 2: f"mpcqp::ric::ric_solve_kernel<{N}>",
-                       3: f"mpcqp::wv::wave_kernel<{N}>"}[eff]
+                       3: f"mpcqp::wv::scale_kernel<{N}> + mpcqp::wv::wave_kernel<{N}>"}[eff]
         traffic = load_traffic(key, kernel_name)
         out = {
             "metric": METRIC,

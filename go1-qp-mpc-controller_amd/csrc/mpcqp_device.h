@@ -107,16 +107,33 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
+// Partner of every lane in the other DPP row of its pair (lane ^ 16) / other row pair (lane ^ 32),
+// through the gfx950 row-swap permutes (no LDS round trip, unlike ds_bpermute).
+__device__ __forceinline__ double xor16(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto l2 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h2 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  // even rows: the odd partner moved into src; odd rows: the even partner moved into vdst
+  const bool odd = (threadIdx.x >> 4) & 1;
+  return __hiloint2double((int)(odd ? h2[0] : h2[1]), (int)(odd ? l2[0] : l2[1]));
+}
+__device__ __forceinline__ double xor32(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const bool upper = (threadIdx.x >> 5) & 1;
+  return __hiloint2double((int)(upper ? h2[0] : h2[1]), (int)(upper ? l2[0] : l2[1]));
+}
 __device__ __forceinline__ double wave_max(double v) {
   v = g16_max(v);
-  v = dmax(v, __shfl_xor(v, 16));
-  v = dmax(v, __shfl_xor(v, 32));
+  v = dmax(v, xor16(v));
+  v = dmax(v, xor32(v));
   return v;
 }
 __device__ __forceinline__ double wave_sum(double v) {
   v = g16_sum(v);
-  v = v + __shfl_xor(v, 16);
-  v = v + __shfl_xor(v, 32);
+  v = v + xor16(v);
+  v = v + xor32(v);
   return v;
 }
 

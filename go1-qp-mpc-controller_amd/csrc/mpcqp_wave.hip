@@ -75,12 +75,10 @@ struct WSmem {
       double Ap[2][C::m];  // unscaled A entries per row: [0] on fx / fy (rows 0-3), [1] on fz
       double qn[C::n];     // this tick's gradient (warm start: q of the Ruiz passes is the old one)
     } h;
-    struct Fs {  // solve: per-step factors + factorization scratch
+    struct Fs {  // solve: per-step factors (the factorization itself runs in registers)
       alignas(16) double Gi[N][144];
       alignas(16) double K[NK][144];
       alignas(16) double Acl[NA][144];
-      alignas(16) double P[144], PA[144], F[144];
-      alignas(16) double xch[2][36];  // block Gauss-Jordan pivot block rows (double-buffered)
       double Rt[N][4][6];             // R'_k foot blocks, upper triangle (00 01 02 11 12 22)
     } f;
   } u;
@@ -364,166 +362,136 @@ __device__ __forceinline__ double quad_at(double v, double v4, double AK0, doubl
   return a < 2 ? s01 : s2;
 }
 
-// ---- factorization of c B'Q̄B + R' (one wave; R' in F.Rt) ------------------------------------------
-// Lanes 0..47 own (row i = t / 4, foot-column block g = t % 4): entries [i][3g..3g+2] of every 12x12
-// product, so the four lanes of row i form a quad and the 3x3 block (i / 3, g) is a foot block.
-// G^-1 is a block Gauss-Jordan with the 3x3 foot blocks as pivots: the pivot block row goes
-// through LDS (one wave-sync per pivot), the pivot column is a quad broadcast.
-__device__ __forceinline__ void inv3(const double (&M)[9], double (&I)[9]) {  // Eigen-style cofactor inverse
-  auto cof = [&](int i, int j) __attribute__((always_inline)) {
-    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-    return M[i1 * 3 + j1] * M[i2 * 3 + j2] - M[i1 * 3 + j2] * M[i2 * 3 + j1];
-  };
-  const double det = (cof(0, 0) * M[0] + cof(1, 0) * M[3]) + cof(2, 0) * M[6];
-  const double id = 1.0 / det;
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) I[j * 3 + i] = cof(i, j) * id;
-}
-
 // index of (r, c) in a symmetric 3x3 stored as its upper triangle 00 01 02 11 12 22
 __device__ __forceinline__ int sym6(int r, int c) {
   const int lo = r < c ? r : c, hi = r < c ? c : r;
   return lo == 0 ? hi : (lo == 1 ? 2 + hi : 5);
 }
-// quad broadcast of lane j (j a constant after unrolling)
-__device__ __forceinline__ double qbcast(double v, int j) {
-  switch (j) {
-    case 0: return dpp<0x00>(v);
-    case 1: return dpp<0x55>(v);
-    case 2: return dpp<0xAA>(v);
-    default: return dpp<0xFF>(v);
-  }
+
+// ---- factorization on the matrix cores -------------------------------------------------------------
+// Every 12x12 product of the Riccati step runs as 16x16 (zero-padded) v_mfma_f64_16x16x4f64 (IEEE
+// binary64 FMAs).  Matrices live in the MFMA result ("D") layout: lane j + 16 g, register v holds
+// row 4v + g, column j.  In that layout register kb of a matrix X is exactly the B operand of K-block
+// kb (X[4kb + kk][j] at lane j + 16 kk) and the A operand of K-block kb of X' (X'[i][4kb + kk] at
+// lane i + 16 kk), so products chain without any data movement: C = A X takes A' and X in D layout.
+typedef double mf4 __attribute__((ext_vector_type(4)));
+
+struct Dm {  // a 16x16 matrix in D layout
+  mf4 r;
+};
+// C (+)= (Aᵀ given as `at`)ᵀ X over K-blocks KB0..KB1-1
+template <int KB0, int KB1>
+__device__ __forceinline__ mf4 mfma_chain(const mf4& at, const mf4& x, mf4 c) {
+#pragma unroll
+  for (int kb = KB0; kb < KB1; ++kb) c = __builtin_amdgcn_mfma_f64_16x16x4f64(at[kb], x[kb], c, 0, 0, 0);
+  return c;
+}
+// value of lane group GP (same lane within the group) in every group
+template <int GP>
+__device__ __forceinline__ double bcast_group(double x) {
+  const int g = threadIdx.x >> 4;
+  const double y = xor16(x);  // group g ^ 1
+  const double z = ((g & 1) == (GP & 1)) ? x : y;
+  const double w = xor32(z);  // group g ^ 2
+  return ((g & 2) == (GP & 2)) ? z : w;
+}
+// lane L of the lane's DPP row (exact: 0 + 1 * x; a -0 becomes +0)
+template <int L>
+__device__ __forceinline__ double rbcast(double x, double one) {
+  double acc = 0.0;
+  asm("s_nop 4\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+      : "+v"(acc)
+      : "v"(x), "v"(one), "i"(L));
+  return acc;
+}
+// In-place Gauss-Jordan inverse of the symmetric positive definite leading 12x12 block (scalar
+// pivots, no pivoting: stable for SPD).  Pad rows / columns 12-15 must hold the identity.
+__device__ __forceinline__ void gj_inverse12(mf4& g) {
+  const int j = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const double one = 1.0;
+  sfor<0, 12>([&](auto P) __attribute__((always_inline)) {
+    constexpr int p = decltype(P)::value, vp = p / 4, gp = p % 4;
+    const double rowp = bcast_group<gp>(g[vp]);  // G[p][j]
+    const double piv = rbcast<p>(rowp, one);     // G[p][p]
+    const double pinv = 1.0 / piv;
+    const double rs = rowp * pinv;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const double col = rbcast<p>(g[v], one);  // G[4v + grp][p]
+      const bool prow = (4 * v + grp) == p;
+      const double upd = (j == p) ? -col * pinv : g[v] - col * rs;
+      const double rowv = (j == p) ? pinv : rs;
+      g[v] = prow ? rowv : upd;
+    }
+  });
 }
 
+// The Riccati recursion of c B'Q̄B + R' (R'_k foot blocks in F.Rt) -> G_k^-1, K_k, Acl_k in LDS.
 template <int N>
-__device__ void factorize(WSmem<N>& sm, const mpcqp_params& p, const Adisc& A, double c, double dtm) {
+__device__ void factorize_mfma(WSmem<N>& sm, const mpcqp_params& p, const Adisc& A, double c, double dtm) {
   auto& F = sm.u.f;
-  const int t = threadIdx.x;
-  const bool act = t < 48;
-  const int i = act ? t >> 2 : 11, g = t & 3, ib = i / 3;
-  for (int e = t; e < 144; e += NT) {
-    const int r = e / 12, j = e % 12;
-    F.P[e] = (r == j) ? c * (2.0 * p.q_weights[r]) : 0.0;
+  const int j = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  mf4 Ad, At, cQ, P;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int u = 4 * v + grp;
+    const bool in = u < 12 && j < 12;
+    Ad[v] = in ? A.at(u, j) : 0.0;
+    At[v] = in ? A.at(j, u) : 0.0;
+    cQ[v] = (in && u == j) ? c * (2.0 * p.q_weights[u]) : 0.0;
+    P[v] = cQ[v];
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    // B_k (rows 6-8: B_w, rows 9-11: dt/m on the matching force component) and B_k', D layout
+    mf4 Bk, Bt, G;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int u = 4 * v + grp;
+      auto bsc = [&](int s, int cc) __attribute__((always_inline)) {  // B_k[s][cc]
+        if (cc >= 12) return 0.0;
+        if (s >= 6 && s < 9) return sm.Bw[k][s - 6][cc];
+        if (s >= 9 && s < 12) return (cc % 3 == s - 9) ? dtm : 0.0;
+        return 0.0;
+      };
+      Bk[v] = bsc(u, j);
+      Bt[v] = bsc(j, u);
+      // R'_k: 3x3 foot blocks (upper triangle stored); identity on the pad
+      double rv = 0.0;
+      if (u < 12 && j < 12 && u / 3 == j / 3) rv = F.Rt[k][u / 3][sym6(u % 3, j % 3)];
+      if (u >= 12 && u == j) rv = 1.0;
+      G[v] = rv;
+    }
+    const mf4 zero = {0.0, 0.0, 0.0, 0.0};
+    // G = R' + B'(P B): P B needs only B's rows 6-11 (K-blocks 1, 2); B' P B likewise
+    const mf4 PB = mfma_chain<1, 3>(P, Bk, zero);
+    G = mfma_chain<1, 3>(Bk, PB, G);
+    gj_inverse12(G);
+    if (j < 12)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) F.Gi[k][12 * (4 * v + grp) + j] = G[v];
+    if (k >= 1) {
+      const mf4 PA = mfma_chain<0, 3>(P, Ad, zero);         // P A
+      const mf4 Fm = mfma_chain<1, 3>(Bk, PA, zero);        // F = B' P A
+      const mf4 K = mfma_chain<0, 3>(G, Fm, zero);          // K = G^-1 F
+      if (j < 12)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) F.K[k - 1][12 * (4 * v + grp) + j] = K[v];
+      if (k <= N - 2) {
+        mf4 nBt;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) nBt[v] = -Bt[v];
+        const mf4 Acl = mfma_chain<0, 3>(nBt, K, Ad);       // A - B K
+        if (j < 12)
+#pragma unroll
+          for (int v = 0; v < 3; ++v) F.Acl[k - 1][12 * (4 * v + grp) + j] = Acl[v];
+      }
+      mf4 nF;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) nF[v] = -Fm[v];
+      P = mfma_chain<0, 3>(nF, K, mfma_chain<0, 3>(Ad, PA, cQ));  // cQ + A'PA - F'K
+    }
   }
   wave_sync();
-  for (int k = N - 1; k >= 0; --k) {
-    // B_k column i (rows 6, 7, 8 and 9 + i%3) and, per owned column cc, B_k column cc
-    const double bi0 = sm.Bw[k][0][i], bi1 = sm.Bw[k][1][i], bi2 = sm.Bw[k][2][i];
-    const int si = 9 + i % 3;
-    double Gv[3], PAv[3];
-#pragma unroll
-    for (int jj = 0; jj < 3; ++jj) {
-      const int cc = 3 * g + jj;
-      const double bc0 = sm.Bw[k][0][cc], bc1 = sm.Bw[k][1][cc], bc2 = sm.Bw[k][2][cc];
-      auto pb = [&](int s) __attribute__((always_inline)) {  // (P B_k)[s][cc]
-        const double* pr = F.P + 12 * s;
-        return ((pr[6] * bc0 + pr[7] * bc1) + pr[8] * bc2) + pr[9 + jj] * dtm;
-      };
-      const double gs = ((bi0 * pb(6) + bi1 * pb(7)) + bi2 * pb(8)) + dtm * pb(si);
-      Gv[jj] = ((ib == g) ? F.Rt[k][ib][sym6(i % 3, jj)] : 0.0) + gs;  // G = R'_k + B_k' P B_k
-      PAv[jj] = A.ma(F.P, i, cc);                         // P A
-    }
-    if (k >= 1 && act)
-#pragma unroll
-      for (int jj = 0; jj < 3; ++jj) F.PA[12 * i + 3 * g + jj] = PAv[jj];
-    // block Gauss-Jordan: G <- G^-1
-#pragma unroll
-    for (int pv = 0; pv < 4; ++pv) {
-      double* xb = F.xch[pv & 1];
-      if (act && ib == pv)
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj) xb[12 * (i % 3) + 3 * g + jj] = Gv[jj];
-      wave_sync();
-      double Mpp[9], Pinv[9], Mpg[9];
-#pragma unroll
-      for (int e = 0; e < 9; ++e) {
-        Mpp[e] = xb[12 * (e / 3) + 3 * pv + e % 3];
-        Mpg[e] = xb[12 * (e / 3) + 3 * g + e % 3];
-      }
-      inv3(Mpp, Pinv);
-      // my row of block (ib, pv): quad broadcast of lane pv
-      double gi[3];
-#pragma unroll
-      for (int jj = 0; jj < 3; ++jj) gi[jj] = qbcast(Gv[jj], pv);
-      const int rr = i % 3;
-      if (ib == pv) {
-        const double pi0 = sel3(rr, Pinv[0], Pinv[3], Pinv[6]), pi1 = sel3(rr, Pinv[1], Pinv[4], Pinv[7]),
-                     pi2 = sel3(rr, Pinv[2], Pinv[5], Pinv[8]);
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj) {
-          const double pr = (pi0 * Mpg[jj] + pi1 * Mpg[3 + jj]) + pi2 * Mpg[6 + jj];
-          Gv[jj] = (g == pv) ? sel3(jj, pi0, pi1, pi2) : pr;
-        }
-      } else {
-        double W[3];
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj) W[jj] = (gi[0] * Pinv[jj] + gi[1] * Pinv[3 + jj]) + gi[2] * Pinv[6 + jj];
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj) {
-          const double up = Gv[jj] - ((W[0] * Mpg[jj] + W[1] * Mpg[3 + jj]) + W[2] * Mpg[6 + jj]);
-          Gv[jj] = (g == pv) ? -W[jj] : up;
-        }
-      }
-    }
-    if (act)
-#pragma unroll
-      for (int jj = 0; jj < 3; ++jj) F.Gi[k][12 * i + 3 * g + jj] = Gv[jj];
-    wave_sync();
-    if (k >= 1) {
-      // F = B_k' P A
-      double Fv[3];
-#pragma unroll
-      for (int jj = 0; jj < 3; ++jj) {
-        const int cc = 3 * g + jj;
-        Fv[jj] = ((bi0 * F.PA[72 + cc] + bi1 * F.PA[84 + cc]) + bi2 * F.PA[96 + cc]) + dtm * F.PA[12 * si + cc];
-      }
-      if (act)
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj) F.F[12 * i + 3 * g + jj] = Fv[jj];
-      wave_sync();
-      // K_k = G^-1 F
-      double gr[12];
-      ld12(gr, &F.Gi[k][12 * i]);
-      double Kv[3];
-#pragma unroll 1
-      for (int jj = 0; jj < 3; ++jj) {
-        double s = 0.0;
-#pragma unroll
-        for (int q = 0; q < 12; ++q) s += gr[q] * F.F[12 * q + 3 * g + jj];
-        Kv[jj] = s;
-      }
-      double* Kk = F.K[k - 1];
-      if (act)
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj) Kk[12 * i + 3 * g + jj] = Kv[jj];
-      wave_sync();
-      // Acl_k = A - B_k K_k ; P_k = cQ + A'(PA) - F' K_k
-#pragma unroll 1
-      for (int jj = 0; jj < 3; ++jj) {
-        const int cc = 3 * g + jj;
-        double bk = 0.0;
-        if (i >= 6 && i < 9) {
-          const double* bw = sm.Bw[k][i - 6];
-#pragma unroll
-          for (int q = 0; q < 12; ++q) bk += bw[q] * Kk[12 * q + cc];
-        } else if (i >= 9) {
-          const int a3 = i - 9;
-          bk = dtm * (((Kk[12 * a3 + cc] + Kk[12 * (3 + a3) + cc]) + Kk[12 * (6 + a3) + cc]) + Kk[12 * (9 + a3) + cc]);
-        }
-        double fk = 0.0;
-#pragma unroll
-        for (int q = 0; q < 12; ++q) fk += F.F[12 * q + i] * Kk[12 * q + cc];
-        const double pn = (((i == cc) ? c * (2.0 * p.q_weights[i]) : 0.0) + A.atm(F.PA, i, cc)) - fk;
-        if (act) {
-          if (k <= N - 2) F.Acl[k - 1][12 * i + cc] = A.at(i, cc) - bk;
-          F.P[12 * i + cc] = pn;
-        }
-      }
-      wave_sync();
-    }
-  }
 }
 
 // ---- OSQP scale_data (scaling.c) as a kernel of its own -------------------------------------------
@@ -1147,8 +1115,12 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     const bool eq = U4[r] - L4[r] < RHO_TOL;
     return loose ? RHO_MIN : (eq ? RHO_EQ_OVER_RHO_INEQ * rho : rho);
   };
+  double RI4[R];  // 1 / rho of row 4 (OSQP rho_inv_vec), refreshed with rho
 #pragma unroll
-  for (int r = 0; r < R; ++r) RHO4[r] = rho4_of(r, rho0);
+  for (int r = 0; r < R; ++r) {
+    RHO4[r] = rho4_of(r, rho0);
+    RI4[r] = 1. / RHO4[r];
+  }
   if (mode != 0) {
     // P~x of the warm iterate (the loop carries P~x through the KKT identity from here):
     // P~x = c D H (D x), H v = B_qp' Q B_qp v + R v by the dynamics: x_{i+1} = A x_i + B_i v_i
@@ -1204,7 +1176,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 
   // ---- 5. ADMM (osqp_solve) ------------------------------------------------------------------------
   auto& F = sm.u.f;
-  double rho = rho0, pri_res = 0.0, dua_res = 0.0;
+  double rho = rho0, rinv = 1. / rho0, pri_res = 0.0, dua_res = 0.0;
   int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
   bool need_factor = true;
   int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
@@ -1242,7 +1214,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         }
       }
       wave_sync();
-      factorize<N>(sm, p, A, cost_c, dtm);
+      factorize_mfma<N>(sm, p, A, cost_c, dtm);
       wave_sync();
       need_factor = false;
       WV_MARK(12);
@@ -1365,16 +1337,15 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     const bool need_info = is_check || is_adapt || last;
 
     // ---- update_x / update_z / update_y, and P~x by the KKT identity P~x~ = rhs - sigma x~ - A~'rho A~x~
-    const double rinv = 1. / rho;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const double xt = DI[r] * U[r];
       const double xp = dpp<QP_PRIM>(xt), xz = dpp<QP_B2>(xt);
       const double zt = AK0[r] * xp + AK1[r] * xz;
       const double zt4 = AK4[r] * xz;
-      {
+      {  // (fmin/fmax = the reference's c_min/c_max on these non-NaN operands)
         const double zr = alpha * zt + (1.0 - alpha) * Z[r];
-        const double zn = dmin(dmax(zr + rinv * Y[r], lo03(r)), hi03(r));
+        const double zn = fmin(fmax(zr + rinv * Y[r], lo03(r)), hi03(r));
         const double dyv = rho * (zr - zn);
         Z[r] = zn;
         Y[r] = Y[r] + dyv;
@@ -1383,22 +1354,21 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       {
         const double r4 = RHO4[r];
         const double zr = alpha * zt4 + (1.0 - alpha) * Z4[r];
-        const double zn = dmin(dmax(zr + (1. / r4) * Y4[r], L4[r]), U4[r]);
+        const double zn = fmin(fmax(zr + RI4[r] * Y4[r], L4[r]), U4[r]);
         const double dyv = r4 * (zr - zn);
         Z4[r] = zn;
         Y4[r] = Y4[r] + dyv;
         DY4[r] = dyv;
       }
       const double kd = quad_at(rho * zt, RHO4[r] * zt4, AK0[r], AK1[r], AK4[r], a);
-      if (vvr[r]) {
-        const double xo = X[r];
-        const double xn = alpha * xt + (1.0 - alpha) * xo;
-        DX[r] = xn - xo;
-        X[r] = xn;
-        const double pxt = (RHS[r] - sigma * xt) - kd;
-        PXO[r] = PX[r];
-        PX[r] = alpha * pxt + (1.0 - alpha) * PX[r];
-      }
+      // every lane updates (values of padding lanes / steps past N are never read unmasked)
+      const double xo = X[r];
+      const double xn = alpha * xt + (1.0 - alpha) * xo;
+      DX[r] = xn - xo;
+      X[r] = xn;
+      const double pxt = (RHS[r] - sigma * xt) - kd;
+      PXO[r] = PX[r];
+      PX[r] = alpha * pxt + (1.0 - alpha) * PX[r];
     }
 
     if (tm_it) WV_MARK(46);
@@ -1565,7 +1535,11 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       if (done) break;
       if (refactor) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) RHO4[r] = rho4_of(r, rho);
+        for (int r = 0; r < R; ++r) {
+          RHO4[r] = rho4_of(r, rho);
+          RI4[r] = 1. / RHO4[r];
+        }
+        rinv = 1. / rho;
         need_factor = true;
       }
     }

@@ -47,27 +47,35 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--key", default="N10_B4096_trot")
-    ap.add_argument("--kernel", default="wave_kernel")  # the default path's kernel
+    ap.add_argument("--kernel", default="scale_kernel,wave_kernel",
+                    help="comma-separated kernel-name substrings; per-launch means are summed (one solve)")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
-    per, names = parse(a.dir, a.kernel)
+    kernels = [k for k in a.kernel.split(",") if k]
+    fetch_kib = write_kib = 0.0
+    knames, ndisp = [], []
+    for kname in kernels:
+        per, names = parse(a.dir, kname)
 
-    def mean_of(counter):
-        vals = [v[counter] for v in per.values() if counter in v]
-        if not vals:
-            print(f"no dispatch with {counter}", file=sys.stderr)
-            sys.exit(1)
-        vals = vals[1:] if len(vals) > 1 else vals  # drop the first (cold) dispatch
-        return sum(vals) / len(vals), len(vals)
+        def mean_of(counter):
+            vals = [v[counter] for v in per.values() if counter in v]
+            if not vals:
+                print(f"no dispatch of {kname} with {counter}", file=sys.stderr)
+                sys.exit(1)
+            vals = vals[1:] if len(vals) > 1 else vals  # drop the first (cold) dispatch
+            return sum(vals) / len(vals), len(vals)
 
-    fetch_kib, nf = mean_of("FETCH_SIZE")
-    write_kib, nw = mean_of("WRITE_SIZE")
-    rows = [None] * min(nf, nw)
+        f_kib, nf = mean_of("FETCH_SIZE")
+        w_kib, nw = mean_of("WRITE_SIZE")
+        fetch_kib += f_kib
+        write_kib += w_kib
+        knames.append(sorted(set(names.values()))[0])
+        ndisp.append(min(nf, nw))
     fetch_b = fetch_kib * 1024.0 * 2.0  # gfx950: FETCH_SIZE counts half of the bytes
     write_b = write_kib * 1024.0
     entry = {
-        "kernel": sorted(set(names.values()))[0],
-        "dispatches": len(rows),
+        "kernel": " + ".join(knames),
+        "dispatches": min(ndisp),
         "fetch_size_kib_raw": fetch_kib,
         "write_size_kib_raw": write_kib,
         "fetch_bytes_corrected": fetch_b,
