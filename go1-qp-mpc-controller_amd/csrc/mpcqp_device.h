@@ -66,10 +66,11 @@ __device__ __forceinline__ double limit_scaling(double d) {
 // ---- cross-lane helpers ----------------------------------------------------------------------
 // DPP move of a double inside a 16-lane row.  CTRL: 0x140 row_mirror (i <-> 15-i),
 // 0x141 row_half_mirror (i <-> 7-i in each half), 0x4E quad_perm xor 2, 0xB1 quad_perm xor 1.
+// (mov_dpp: no "old" operand to materialize; every control used here reads an in-row lane)
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
 // 16-lane all-reduce; the four pairings generate the whole group and every step adds the same two

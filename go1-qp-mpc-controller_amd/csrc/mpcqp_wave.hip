@@ -1171,6 +1171,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   }
   // rows 0-3: l = 0 / u = +inf (rows 0, 2) or l = -inf / u = 0 (rows 1, 3): always inequalities
   auto lo03 = [&](int r) __attribute__((always_inline)) { return (a & 1) ? Ev[r] * -OSQP_INF : Ev[r] * 0.0; };
+  // the projection onto those bounds needs no E: [0, +inf) for rows 0, 2, (-inf, 0] for rows 1, 3
+  // (equal to clamping at E * -+OSQP_INF for every operand below 1e30 E in magnitude)
+  const double LO03 = (a & 1) ? -INFINITY : 0.0, HI03 = (a & 1) ? 0.0 : INFINITY;
   auto hi03 = [&](int r) __attribute__((always_inline)) { return (a & 1) ? Ev[r] * 0.0 : Ev[r] * OSQP_INF; };
   wave_sync();  // every LDS read of the setup image precedes its reuse by the factorization
 
@@ -1345,7 +1348,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       const double zt4 = AK4[r] * xz;
       {  // (fmin/fmax = the reference's c_min/c_max on these non-NaN operands)
         const double zr = alpha * zt + (1.0 - alpha) * Z[r];
-        const double zn = fmin(fmax(zr + rinv * Y[r], lo03(r)), hi03(r));
+        const double zn = fmin(fmax(zr + rinv * Y[r], LO03), HI03);
         const double dyv = rho * (zr - zn);
         Z[r] = zn;
         Y[r] = Y[r] + dyv;
@@ -1546,8 +1549,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     // ---- next right-hand side: sigma x - q~ + A~'(rho z - y) ----
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+      // (padding lanes and steps past N compute values nothing reads unmasked)
       const double at = quad_at(rho * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
-      RHS[r] = vvr[r] ? (sigma * X[r] - Qv[r]) + at : 0.0;
+      RHS[r] = (sigma * X[r] - Qv[r]) + at;
     }
     if (tm_it) WV_MARK(47);
   }
