@@ -203,8 +203,10 @@ def main():
                          "traffic": traffic,
                          "kernel": kernel_name, "kernel_ms": kern_ms,
                          "algorithmic_flop_per_launch": flops,
-                         "note": "binary64 VALU (v_fma_f64 / DPP) bound, no MFMA in this kernel; "
-                                 "peak = FP64 vector spec (equal to the FP64 MFMA peak on gfx950)"},
+                         "note": "binary64; the ADMM iterations (86% of the solve) run on the VALU "
+                                 "(v_fmac_f64 DPP mat-vecs) and bound it, the Riccati factorization "
+                                 "runs on v_mfma_f64_16x16x4f64; peak = FP64 vector spec (equal to "
+                                 "the FP64 MFMA peak on gfx950)"},
             "cpu_baseline": cpu,
             "parity": parity,
             "stats": {"mean_iters": float(res["iters"].mean()), "max_iters": int(res["iters"].max()),
