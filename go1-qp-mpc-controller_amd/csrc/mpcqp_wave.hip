@@ -395,14 +395,24 @@ __device__ __forceinline__ double bcast_group(double x) {
   const double w = xor32(z);  // group g ^ 2
   return ((g & 2) == (GP & 2)) ? z : w;
 }
-// lane L of the lane's DPP row (exact: 0 + 1 * x; a -0 becomes +0)
+// lane L of the lane's DPP row (exact: 0 + 1 * x; a -0 becomes +0).  Used only in straight-line
+// code without EXEC writes, so the DPP source hazard needs 2 wait states, not 5.
 template <int L>
 __device__ __forceinline__ double rbcast(double x, double one) {
   double acc = 0.0;
-  asm("s_nop 4\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+  asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
       : "+v"(acc)
       : "v"(x), "v"(one), "i"(L));
   return acc;
+}
+// 1 / d: hardware reciprocal + two Newton steps (correct to the last bit or one ulp; the pivots of
+// an SPD matrix are positive and normal)
+__device__ __forceinline__ double recip(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
 }
 // In-place Gauss-Jordan inverse of the symmetric positive definite leading 12x12 block (scalar
 // pivots, no pivoting: stable for SPD).  Pad rows / columns 12-15 must hold the identity.
@@ -413,15 +423,15 @@ __device__ __forceinline__ void gj_inverse12(mf4& g) {
     constexpr int p = decltype(P)::value, vp = p / 4, gp = p % 4;
     const double rowp = bcast_group<gp>(g[vp]);  // G[p][j]
     const double piv = rbcast<p>(rowp, one);     // G[p][p]
-    const double pinv = 1.0 / piv;
+    const double pinv = recip(piv);
     const double rs = rowp * pinv;
+    const bool jp = j == p;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const double col = rbcast<p>(g[v], one);  // G[4v + grp][p]
-      const bool prow = (4 * v + grp) == p;
-      const double upd = (j == p) ? -col * pinv : g[v] - col * rs;
-      const double rowv = (j == p) ? pinv : rs;
-      g[v] = prow ? rowv : upd;
+      const double upd = jp ? -col * pinv : g[v] - col * rs;
+      if (v == vp) g[v] = (grp == gp) ? (jp ? pinv : rs) : upd;  // row p
+      else g[v] = upd;
     }
   });
 }
