@@ -540,39 +540,32 @@ struct ScaleSmem {
   using C = Cfg<N>;
   alignas(16) double Bw[N][3][ND];
   double rec[C::REC];
-  double D[C::n], Dt[C::n], q[C::n], qn[C::n], E[C::m];
+  double D[C::n], q[C::n], qn[C::n], E[C::m];
   double lam[N][ND];
   double vec[2][16];
   double Ap[2][C::m];
   double red[2][16];
 };
 
+// block-wide sum of sv and max of qv in one barrier (wave partials summed in wave order)
 template <int NW>
-__device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum(v);
-  if constexpr (NW == 1) {
-    return v;
-  } else {
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+__device__ __forceinline__ void block_sum_max(double& sv, double& qv, double (*red)[16]) {
+  sv = wave_sum(sv);
+  qv = wave_max(qv);
+  if constexpr (NW > 1) {
+    if ((threadIdx.x & 63) == 0) {
+      red[0][threadIdx.x >> 6] = sv;
+      red[1][threadIdx.x >> 6] = qv;
+    }
     __syncthreads();
-    double s = red[0];
+    double s = red[0][0], q = red[1][0];
 #pragma unroll
-    for (int i = 1; i < NW; ++i) s += red[i];
-    return s;
-  }
-}
-template <int NW>
-__device__ __forceinline__ double block_max(double v, double* red) {
-  v = wave_max(v);
-  if constexpr (NW == 1) {
-    return v;
-  } else {
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    double s = red[0];
-#pragma unroll
-    for (int i = 1; i < NW; ++i) s = fmax(s, red[i]);
-    return s;
+    for (int i = 1; i < NW; ++i) {
+      s += red[0][i];
+      q = fmax(q, red[1][i]);
+    }
+    sv = s;
+    qv = q;
   }
 }
 
@@ -714,27 +707,31 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
       sm.Bw[k][rr][cc] = s * dt;
     }
     // forward: a_i = A_d^{i+1} x0 (13 states), e_i = 2q (a_i - x_ref_i); backward: lambda_j = e_j + A' lambda_{j+1}
-    if (t < SD) sm.vec[0][t] = rec[MPCQP_REC_X0 + t];
-    __syncthreads();
-    for (int i = 0; i < N; ++i) {
-      if (t < SD) {
-        const double* pv = sm.vec[i & 1];
-        double s;
-        if (t == 0) s = (pv[0] + A.ad0 * pv[6]) + A.ad1 * pv[7];
-        else if (t == 1) s = (pv[1] + (-A.ad1) * pv[6]) + A.ad0 * pv[7];
-        else if (t == 2) s = pv[2] + dt * pv[8];
-        else if (t <= 5) s = pv[t] + dt * pv[t + 6];
-        else if (t == 11) s = pv[11] + dt * pv[12];
-        else s = pv[t];
-        sm.vec[(i + 1) & 1][t] = s;
-        if (t < ND) sm.lam[i][t] = 2 * p.q_weights[t] * (s - rec[MPCQP_REC_XREF + SD * i + t]);
+    // (sequential over the horizon: wave 0 alone, wave-synchronous; one block barrier at the end)
+    if (t < 64) {
+      if (t < SD) sm.vec[0][t] = rec[MPCQP_REC_X0 + t];
+      wave_sync();
+      for (int i = 0; i < N; ++i) {
+        if (t < SD) {
+          const double* pv = sm.vec[i & 1];
+          double s;
+          if (t == 0) s = (pv[0] + A.ad0 * pv[6]) + A.ad1 * pv[7];
+          else if (t == 1) s = (pv[1] + (-A.ad1) * pv[6]) + A.ad0 * pv[7];
+          else if (t == 2) s = pv[2] + dt * pv[8];
+          else if (t <= 5) s = pv[t] + dt * pv[t + 6];
+          else if (t == 11) s = pv[11] + dt * pv[12];
+          else s = pv[t];
+          sm.vec[(i + 1) & 1][t] = s;
+          if (t < ND) sm.lam[i][t] = 2 * p.q_weights[t] * (s - rec[MPCQP_REC_XREF + SD * i + t]);
+        }
+        wave_sync();
       }
-      __syncthreads();
+      for (int j = N - 2; j >= 0; --j) {
+        if (t < ND) sm.lam[j][t] = sm.lam[j][t] + A.atv(t, sm.lam[j + 1]);
+        wave_sync();
+      }
     }
-    for (int j = N - 2; j >= 0; --j) {
-      if (t < ND) sm.lam[j][t] = sm.lam[j][t] + A.atv(t, sm.lam[j + 1]);
-      __syncthreads();
-    }
+    __syncthreads();
   }
   // thread t: column j0 = t / 4, blocks jb .. jb+BPT-1 of it (the column's four threads are a quad)
   constexpr int BPT = SC::BPT;
@@ -883,9 +880,11 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     __syncthreads();
   }
   for (int pass = 0; pass < p.scaling; ++pass) {
+    // new scaling factors from the current D, E (every thread reads before anyone writes)
+    double dtv = 1.0;
     if (lead && j0 < n) {
       const double pc = (c_s * sm.D[j0]) * cm;
-      sm.Dt[j0] = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j0))));
+      dtv = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j0))));
     }
     double et[SC::RPT];
 #pragma unroll
@@ -900,8 +899,8 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
       if (r < m) sm.E[r] *= et[rr];
     }
     if (lead && j0 < n) {
-      sm.q[j0] = sm.Dt[j0] * sm.q[j0];
-      sm.D[j0] = sm.D[j0] * sm.Dt[j0];
+      sm.q[j0] = dtv * sm.q[j0];
+      sm.D[j0] = sm.D[j0] * dtv;
     }
     __syncthreads();
     cm = colmax(false);  // column norms of the D-scaled P (cost normalization)
@@ -910,17 +909,16 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
       sv = (c_s * sm.D[j0]) * cm;
       qv = dabs(sm.q[j0]);
     }
-    sv = block_sum<SC::NWS>(sv, sm.red[0]);
-    qv = block_max<SC::NWS>(qv, sm.red[1]);
+    block_sum_max<SC::NWS>(sv, qv, sm.red);
     double c_temp = sv / n;
     const double inf_norm_q = limit_scaling(qv);
     c_temp = dmax(c_temp, inf_norm_q);
     c_temp = limit_scaling(c_temp);
     c_temp = 1. / c_temp;
-    if (lead && j0 < n) sm.q[j0] *= c_temp;
+    if (lead && j0 < n) sm.q[j0] *= c_temp;  // own column only: no barrier before the next pass
     c_s *= c_temp;
-    __syncthreads();
   }
+  __syncthreads();
   double* out = img + (size_t)inst * SI::SIZE;
   if (lead && j0 < n) {
     out[SI::D + j0] = sm.D[j0];
