@@ -22,7 +22,7 @@ struct mpcqp_handle {
   double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
   size_t work_per = 0;       // doubles per instance the workspace was sized for
-  int path = 0;              // 0 auto, 1 dense K^-1, 2 Riccati workgroup, 3 Riccati wave (mpcqp_debug_set_solver)
+  int path = 0;              // 0 auto, 1 dense K^-1, 2 Riccati workgroup, 3 Riccati wave, 4 wave per round (mpcqp_debug_set_solver)
   // host wrapper staging
   double* d_recs = nullptr;
   mpcqp_result* d_res = nullptr;
@@ -72,7 +72,8 @@ bool params_valid(const mpcqp_params* p) {
   return true;
 }
 
-// 1 dense K^-1, 2 Riccati (one workgroup per robot), 3 Riccati (one wave per robot)
+// 1 dense K^-1, 2 Riccati (one workgroup per robot), 3 Riccati (one wave per robot), 4 Riccati (one
+// wave per horizon round)
 int effective_path(const mpcqp_handle* h) {
   if (h->path != 0) return h->path;
   return h->p.horizon <= mpcqp::WAVE_MAX_HORIZON ? 3 : 2;
@@ -88,7 +89,8 @@ hipError_t occupancy_for(const mpcqp_handle* h, int* per_cu) {
   switch (effective_path(h)) {
     case 1: return mpcqp::occupancy_any(h->p.horizon, per_cu);
     case 2: return mpcqp::occupancy_riccati_any(h->p.horizon, per_cu);
-    default: return mpcqp::occupancy_wave_any(h->p.horizon, per_cu);
+    case 3: return mpcqp::occupancy_wave_any(h->p.horizon, per_cu);
+    default: return mpcqp::occupancy_mw_any(h->p.horizon, per_cu);
   }
 }
 // (Re)size the per-instance workspace for `batch` instances of the current path.
@@ -187,7 +189,7 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
                                  mpcqp_result* d_results, double* d_solution, double* d_trace,
                                  int32_t trace_cap, void* stream, double* d_state = nullptr) {
   if (!h || batch < 0 || (batch > 0 && (!d_records || !d_results))) return MPCQP_ERR_INVALID_ARG;
-  if (d_state && effective_path(h) != 3) return MPCQP_ERR_INVALID_ARG;  // warm start: wave path only
+  if (d_state && effective_path(h) < 3) return MPCQP_ERR_INVALID_ARG;  // warm start: wave paths only
   if (batch == 0) return MPCQP_OK;
   DeviceGuard dg(h->device);
   hipError_t e = dg.err;
@@ -210,7 +212,8 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   switch (effective_path(h)) {
     case 1: e = mpcqp::launch_solve_any(a); break;
     case 2: e = mpcqp::launch_riccati_any(a); break;
-    default: e = mpcqp::launch_wave_any(a); break;
+    case 3: e = mpcqp::launch_wave_any(a); break;
+    default: e = mpcqp::launch_mw_any(a); break;
   }
   if (e != hipSuccess) return set_hip_error(h, e, "solve_kernel launch");
   return MPCQP_OK;
@@ -407,9 +410,9 @@ int32_t mpcqp_solve_threads(int32_t horizon) {
 }
 
 int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
-  if (!h || path < 0 || path > 3) return MPCQP_ERR_INVALID_ARG;
+  if (!h || path < 0 || path > 4) return MPCQP_ERR_INVALID_ARG;
   if (path == 1 && h->p.horizon > mpcqp::DENSE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
-  if (path == 3 && h->p.horizon > mpcqp::WAVE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
+  if (path >= 3 && h->p.horizon > mpcqp::WAVE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
   DeviceGuard dg(h->device);
   hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");

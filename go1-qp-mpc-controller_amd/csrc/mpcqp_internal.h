@@ -40,6 +40,10 @@ constexpr int DENSE_MAX_HORIZON = 10;
 hipError_t launch_wave_any(const LaunchArgs& a);
 hipError_t occupancy_wave_any(int horizon, int* blocks);
 hipError_t wave_selftest(double* d_out, void* stream);
+hipError_t launch_scale_any(const LaunchArgs& a);  // scale_kernel alone (the image in a.work)
+// Wave-per-round path (mpcqp_wave_mw.hip): scale_kernel + mw_kernel, horizons 1..WAVE_MAX_HORIZON
+hipError_t launch_mw_any(const LaunchArgs& a);
+hipError_t occupancy_mw_any(int horizon, int* blocks);
 constexpr int WAVE_MAX_HORIZON = 20;
 // doubles per robot of the warm-start slot (mpcqp_wave.hip WarmLayout)
 __host__ __device__ constexpr int warm_state_doubles(int N) {

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(PKG_ROOT, "lib", "libmpcq
 STATE_DIM, NUM_LEG, NUM_DOF, CONSTRAINT_DIM = 13, 4, 12, 20
 MAX_HORIZON = 20
 DENSE_MAX_HORIZON = 10  # the dense K^-1 path (debug selection) serves horizons up to this
-SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI, SOLVER_WAVE = 0, 1, 2, 3
+SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI, SOLVER_WAVE, SOLVER_WAVE_MW = 0, 1, 2, 3, 4
 OSQP_INFTY = 1e30
 
 # record layout (include/mpcqp.h MPCQP_REC_*)

@@ -109,6 +109,236 @@ __global__ __launch_bounds__(64) void chain_pf_kernel(double* out, long long* cy
   if (t == 0) cyc[blockIdx.x] = c1 - c0;
 }
 
+
+// y = sum_c M[c] x_c + a  (accumulator a0 starts at `init`: the chain's "- a_k" folded in)
+__device__ __forceinline__ double mv12i(double x, const double (&c)[12], double init) {
+  double a0 = init, a1 = 0.0, a2 = 0.0;
+  asm("s_nop 4\n\t"
+      FM("%[a1]", "%[c1]", 1) FM("%[a2]", "%[c2]", 2) FM("%[a0]", "%[c0]", 0)
+      FM("%[a1]", "%[c4]", 5) FM("%[a2]", "%[c5]", 6) FM("%[a0]", "%[c3]", 4)
+      FM("%[a1]", "%[c7]", 9) FM("%[a2]", "%[c8]", 10) FM("%[a0]", "%[c6]", 8)
+      FM("%[a1]", "%[c10]", 13) FM("%[a2]", "%[c11]", 14) FM("%[a0]", "%[c9]", 12)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
+        [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]),
+        [c11] "v"(c[11]));
+  return (a1 + a2) + a0;
+}
+// odd rows := even rows (other rows undefined): one permlane16_swap per dword, no copies
+__device__ __forceinline__ double to_odd(double v) {
+  unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  unsigned rl, rh;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3"
+               : "=&v"(rl), "=&v"(rh), "+v"(lo), "+v"(hi));
+  return __hiloint2double((int)rh, (int)rl);
+}
+// LDS chain, prefetch pinned by sched_barrier, folded subtraction, copy-free hand-off
+__global__ __launch_bounds__(64) void chain_pf2_kernel(double* out, long long* cyc, int iters) {
+  extern __shared__ double lds[];
+  const int t = threadIdx.x, idx = t & 15;
+  for (int e = t; e < 9 * 144; e += 64) lds[e] = 1e-3 * ((e * 37) % 101) - 0.05;
+  __builtin_amdgcn_wave_barrier();
+  double cur = 0.5 + 0.01 * t;
+  const double ak = 0.125 * t;
+  const double* base = lds + (idx % 12);
+  double cn[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) cn[i] = base[12 * i];
+  const long long c0 = __builtin_readcyclecounter();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      double c[12];
+#pragma unroll
+      for (int i = 0; i < 12; ++i) c[i] = cn[i];
+      const double* p = base + 144 * ((k + 1) % 9);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) cn[i] = p[12 * i];
+      __builtin_amdgcn_sched_barrier(0);
+      cur = mv12i(to_odd(cur), c, -ak);
+    }
+  }
+  const long long c1 = __builtin_readcyclecounter();
+  out[blockIdx.x * 64 + t] = cur;
+  if (t == 0) cyc[blockIdx.x] = c1 - c0;
+}
+// register matrices, folded subtraction, copy-free hand-off (compute floor of the new step)
+__global__ __launch_bounds__(64) void chain_reg2_kernel(double* out, long long* cyc, int iters) {
+  const int t = threadIdx.x;
+  double m[9][12];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int i = 0; i < 12; ++i) m[k][i] = 1e-3 * (((k * 12 + i) * 37 + t) % 101) - 0.05;
+  double cur = 0.5 + 0.01 * t;
+  const double ak = 0.125 * t;
+  const long long c0 = __builtin_readcyclecounter();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) cur = mv12i(to_odd(cur), m[k], -ak);
+  }
+  const long long c1 = __builtin_readcyclecounter();
+  out[blockIdx.x * 64 + t] = cur;
+  if (t == 0) cyc[blockIdx.x] = c1 - c0;
+}
+
+
+// as chain_pf2, the matrix stored transposed so the lane's 12 coefficients are contiguous (b128)
+__global__ __launch_bounds__(64) void chain_pf3_kernel(double* out, long long* cyc, int iters) {
+  extern __shared__ double lds[];
+  const int t = threadIdx.x, idx = t & 15;
+  for (int e = t; e < 9 * 144; e += 64) lds[e] = 1e-3 * ((e * 37) % 101) - 0.05;
+  __builtin_amdgcn_wave_barrier();
+  double cur = 0.5 + 0.01 * t;
+  const double ak = 0.125 * t;
+  const double* base = lds + 12 * (idx % 12);
+  double cn[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) cn[i] = base[i];
+  const long long c0 = __builtin_readcyclecounter();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      double c[12];
+#pragma unroll
+      for (int i = 0; i < 12; ++i) c[i] = cn[i];
+      const double2* p = reinterpret_cast<const double2*>(base + 144 * ((k + 1) % 9));
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double2 v = p[i];
+        cn[2 * i] = v.x;
+        cn[2 * i + 1] = v.y;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      cur = mv12i(to_odd(cur), c, -ak);
+    }
+  }
+  const long long c1 = __builtin_readcyclecounter();
+  out[blockIdx.x * 64 + t] = cur;
+  if (t == 0) cyc[blockIdx.x] = c1 - c0;
+}
+// rows split the 12-term dot product: x rotated per row, 3 DPP FMAs, cross-row all-reduce
+__device__ __forceinline__ double rot_row(double x, int q) {  // row q lanes a <- lanes a + 4q
+  const double r12 = __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x12C, 0xF, 0xF, false),
+                                      __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x12C, 0xF, 0xF, false));
+  const double r8 = __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x128, 0xF, 0xF, false));
+  const double r4 = __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x124, 0xF, 0xF, false),
+                                     __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x124, 0xF, 0xF, false));
+  const double a = (q & 1) ? r12 : x;
+  const double b = (q & 1) ? r4 : r8;
+  return (q & 2) ? b : a;
+}
+__device__ __forceinline__ double rowsum(double p) {
+  unsigned al = (unsigned)__double2loint(p), ah = (unsigned)__double2hiint(p);
+  unsigned bl = al, bh = ah;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3"
+               : "+v"(al), "+v"(ah), "+v"(bl), "+v"(bh));
+  double s = __hiloint2double((int)ah, (int)al) + __hiloint2double((int)bh, (int)bl);
+  al = (unsigned)__double2loint(s); ah = (unsigned)__double2hiint(s);
+  bl = al; bh = ah;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %2\n\tv_permlane32_swap_b32 %1, %3"
+               : "+v"(al), "+v"(ah), "+v"(bl), "+v"(bh));
+  return __hiloint2double((int)ah, (int)al) + __hiloint2double((int)bh, (int)bl);
+}
+__global__ __launch_bounds__(64) void chain_split_kernel(double* out, long long* cyc, int iters) {
+  extern __shared__ double lds[];
+  const int t = threadIdx.x, idx = t & 15, q = t >> 4;
+  for (int e = t; e < 9 * 4 * 48; e += 64) lds[e] = 1e-3 * ((e * 37) % 101) - 0.05;
+  __builtin_amdgcn_wave_barrier();
+  double cur = 0.5 + 0.01 * t;
+  const double ak = 0.125 * t;
+  const double* base = lds + 48 * q + 4 * (idx % 12);  // [k][row q][lane][4]
+  double cn[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) cn[i] = base[i];
+  const long long c0 = __builtin_readcyclecounter();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const double c0_ = cn[0], c1_ = cn[1], c2_ = cn[2];
+      const double* p = base + 192 * ((k + 1) % 9);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) cn[i] = p[i];
+      __builtin_amdgcn_sched_barrier(0);
+      const double xr = rot_row(cur, q);
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+      asm("s_nop 4\n\t"
+          "v_fmac_f64_dpp %[a0], %[x], %[c0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+          "v_fmac_f64_dpp %[a1], %[x], %[c1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_fmac_f64_dpp %[a2], %[x], %[c2] row_newbcast:2 row_mask:0xf bank_mask:0xf"
+          : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+          : [x] "v"(xr), [c0] "v"(c0_), [c1] "v"(c1_), [c2] "v"(c2_));
+      cur = rowsum((a0 + a1) + a2) - ak;
+    }
+  }
+  const long long c1 = __builtin_readcyclecounter();
+  out[blockIdx.x * 64 + t] = cur;
+  if (t == 0) cyc[blockIdx.x] = c1 - c0;
+}
+
+// rows split the 12-term dot product with no rotation: 12 DPP FMAs, each writing only the row that
+// owns its column (row q: columns 3q..3q+2 = lanes 4q..4q+2), then the cross-row all-reduce.
+// Each lane loads 3 coefficients instead of 12 (4x less LDS traffic).
+#define FMR(A, M, L, RM) "v_fmac_f64_dpp " A ", %[x], " M " row_newbcast:" #L " row_mask:" #RM " bank_mask:0xf\n\t"
+__device__ __forceinline__ double mvq(double x, double m0, double m1, double m2, double init) {
+  double a0 = init, a1 = 0.0, a2 = 0.0;
+  asm("s_nop 4\n\t"
+      FMR("%[a1]", "%[c1]", 1, 0x1) FMR("%[a2]", "%[c2]", 2, 0x1) FMR("%[a0]", "%[c0]", 0, 0x1)
+      FMR("%[a1]", "%[c1]", 5, 0x2) FMR("%[a2]", "%[c2]", 6, 0x2) FMR("%[a0]", "%[c0]", 4, 0x2)
+      FMR("%[a1]", "%[c1]", 9, 0x4) FMR("%[a2]", "%[c2]", 10, 0x4) FMR("%[a0]", "%[c0]", 8, 0x4)
+      FMR("%[a1]", "%[c1]", 13, 0x8) FMR("%[a2]", "%[c2]", 14, 0x8) FMR("%[a0]", "%[c0]", 12, 0x8)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [x] "v"(x), [c0] "v"(m0), [c1] "v"(m1), [c2] "v"(m2));
+  return (a1 + a2) + a0;
+}
+__global__ __launch_bounds__(64) void chain_mask_kernel(double* out, long long* cyc, int iters) {
+  extern __shared__ double lds[];
+  const int t = threadIdx.x, idx = t & 15, q = t >> 4;
+  for (int e = t; e < 9 * 4 * 48; e += 64) lds[e] = 1e-3 * ((e * 37) % 101) - 0.05;
+  __builtin_amdgcn_wave_barrier();
+  double cur = 0.5 + 0.01 * t;
+  const double ak = q == 0 ? 0.125 * t : 0.0;
+  const double* base = lds + 48 * q + 4 * (idx % 12);  // [k][row q][lane][4]
+  double cn[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) cn[i] = base[i];
+  const long long c0 = __builtin_readcyclecounter();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const double c0_ = cn[0], c1_ = cn[1], c2_ = cn[2];
+      const double* p = base + 192 * ((k + 1) % 9);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) cn[i] = p[i];
+      __builtin_amdgcn_sched_barrier(0);
+      cur = rowsum(mvq(cur, c0_, c1_, c2_, -ak));
+    }
+  }
+  const long long c1 = __builtin_readcyclecounter();
+  out[blockIdx.x * 64 + t] = cur;
+  if (t == 0) cyc[blockIdx.x] = c1 - c0;
+}
+// as chain_mask with the matrices in registers (compute floor)
+__global__ __launch_bounds__(64) void chain_mask_reg_kernel(double* out, long long* cyc, int iters) {
+  const int t = threadIdx.x, q = t >> 4;
+  double m[9][3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) m[k][i] = 1e-3 * (((k * 12 + i) * 37 + t) % 101) - 0.05;
+  double cur = 0.5 + 0.01 * t;
+  const double ak = q == 0 ? 0.125 * t : 0.0;
+  const long long c0 = __builtin_readcyclecounter();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) cur = rowsum(mvq(cur, m[k][0], m[k][1], m[k][2], -ak));
+  }
+  const long long c1 = __builtin_readcyclecounter();
+  out[blockIdx.x * 64 + t] = cur;
+  if (t == 0) cyc[blockIdx.x] = c1 - c0;
+}
+
 // dependent v_fma_f64 chain (ILP 1) or 8 independent chains (ILP 8)
 template <int ILP>
 __global__ __launch_bounds__(64) void fma_kernel(double* out, long long* cyc, int iters) {
@@ -174,7 +404,7 @@ static void run(const char* name, KFn fn, int waves_per_cu, int iters, double op
   const int blocks = cus * waves_per_cu * 4;  // 4 generations of resident waves
   size_t lds = (160 * 1024) / waves_per_cu;
   lds = lds / 16 * 16;
-  if (lds < 9 * 144 * 8) lds = 9 * 144 * 8;
+  if (lds < 9 * 192 * 8) lds = 9 * 192 * 8;
   double* out;
   long long* cyc;
   CK(hipMalloc(&out, sizeof(double) * 64 * blocks));
@@ -206,9 +436,20 @@ static void run(const char* name, KFn fn, int waves_per_cu, int iters, double op
 
 int main() {
   const int W[] = {4, 8, 12, 16};
+  if (getenv("MB_MASK_ONLY")) {
+    for (int w : W) run("chain_pf3", chain_pf3_kernel, w, 200, 9);
+    for (int w : W) run("chain_reg2", chain_reg2_kernel, w, 200, 9);
+    for (int w : W) run("chain_mask", chain_mask_kernel, w, 200, 9);
+    for (int w : W) run("chain_mask_reg", chain_mask_reg_kernel, w, 200, 9);
+    return 0;
+  }
   for (int w : W) run("chain(step)", chain_kernel, w, 200, 9);
   for (int w : W) run("chain_reg", chain_reg_kernel, w, 200, 9);
   for (int w : W) run("chain_pf", chain_pf_kernel, w, 200, 9);
+  for (int w : W) run("chain_pf2", chain_pf2_kernel, w, 200, 9);
+  for (int w : W) run("chain_reg2", chain_reg2_kernel, w, 200, 9);
+  for (int w : W) run("chain_pf3", chain_pf3_kernel, w, 200, 9);
+  for (int w : W) run("chain_split", chain_split_kernel, w, 200, 9);
   for (int w : W) run("fma dep", fma_kernel<1>, w, 2000, 16);
   for (int w : W) run("fma ilp8", fma_kernel<8>, w, 500, 128);
   for (int w : W) run("dppfma dep", dppfma_kernel<1>, w, 2000, 16);
