@@ -632,10 +632,17 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       }
       double cn[12];
 #pragma unroll
-      for (int r = 0; r < R; ++r) ld12s(cA[r], &F.K[kk[r]][idx]);
-      if constexpr (N >= 3) ld12s(cn, &F.Acl[N - 3][idx]);
+      for (int r = 0; r < R; ++r) ldcol(cA[r], &F.K[kk[r]][idx]);
+      // The chains load Acl one ROUND at a time: DPP row q takes the matrix of step 4 rr + gray(q) of
+      // round rr, the step that row computes (every chain step runs in the row of its step), so one
+      // 12-double load per lane serves four chain steps.
+      constexpr int NA = WSmem<N>::NA;
+      auto aslot = [&](int rr) __attribute__((always_inline)) { return min(max(4 * rr + ig - 1, 0), NA - 1); };
+      if constexpr (N >= 3) ldcol(cn, &F.Acl[aslot((N - 2) >> 2)][idx]);
       __builtin_amdgcn_sched_barrier(0);
       // a_k = K_k' w_k (k >= 1)
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds_wait<N >= 3 ? 12 : 0>(cA[r]);
       mv_rounds<R>(W, cA, AKw);
 #pragma unroll
       for (int r = 0; r < R; ++r) {  // for g_k: G_k^-1 rows and B_k' columns
@@ -648,15 +655,18 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       if (tm_it) WV_MARK(41);
       {  // backward chain: s_{N-1} = -a_{N-1}; s_k = Acl_k' s_{k+1} - a_k; SMv (row of k) = s_{k+1}
         double cur = -AKw[(N - 1) >> 2];
+        double cc[12];
         sfor<0, N - 1>([&](auto J) {
           constexpr int k = N - 2 - decltype(J)::value;
           const double mvv = rmove2<row_of(k + 1), row_of(k)>(cur);
           SMv[k >> 2] = (q == row_of(k)) ? mvv : SMv[k >> 2];
           if constexpr (k >= 1) {
-            double cc[12];
+            if constexpr (k == N - 2 || (k & 3) == 3) {  // entering round k >> 2 (descending)
+              lds_wait<0>(cn);
 #pragma unroll
-            for (int e = 0; e < 12; ++e) cc[e] = cn[e];
-            if constexpr (k >= 2) ld12s(cn, &F.Acl[k - 2][idx]);  // the next step's column
+              for (int e = 0; e < 12; ++e) cc[e] = cn[e];
+              if constexpr (k >= 4) ldcol(cn, &F.Acl[aslot((k >> 2) - 1)][idx]);  // the next round's columns
+            }
             __builtin_amdgcn_sched_barrier(0);
             cur = mv12a(mvv, cc, -AKw[k >> 2]);
           }
@@ -676,7 +686,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       mv_rounds<R>(tt, cB, G);
       // h_k = B_k g_k: rows 6-8 (leg-2 lanes) B_w g, rows 9-11 (leg-3 lanes) dt/m times the sum of
       // the legs' matching force component, rows 0-5 zero
-      if constexpr (N >= 3) ld12(cn, &F.Acl[0][mo(idx)]);
+      if constexpr (N >= 3) ld12(cn, &F.Acl[aslot(0)][mo(idx)]);
 #pragma unroll
       for (int r = 0; r < R; ++r) ld12(cB[r], &F.K[kk[r]][mo(idx)]);  // for u_k
       __builtin_amdgcn_sched_barrier(0);
@@ -692,15 +702,17 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       if (tm_it) WV_MARK(43);
       {  // forward chain: x_1 = h_0; x_{k+1} = Acl_k x_k + h_k; XS (row of k) = x_k
         double cur = Hh[0];
+        double cc[12];
         sfor<1, N>([&](auto K) {
           constexpr int k = decltype(K)::value;
           const double mvv = rmove2<row_of(k - 1), row_of(k)>(cur);
           XS[k >> 2] = (q == row_of(k)) ? mvv : XS[k >> 2];
           if constexpr (k <= N - 2) {
-            double cc[12];
+            if constexpr (k == 1 || (k & 3) == 0) {  // entering round k >> 2 (ascending)
 #pragma unroll
-            for (int e = 0; e < 12; ++e) cc[e] = cn[e];
-            if constexpr (k + 1 <= N - 2) ld12(cn, &F.Acl[k][mo(idx)]);  // the next step's row
+              for (int e = 0; e < 12; ++e) cc[e] = cn[e];
+              if constexpr (4 * ((k >> 2) + 1) <= N - 2) ld12(cn, &F.Acl[aslot((k >> 2) + 1)][mo(idx)]);
+            }
             __builtin_amdgcn_sched_barrier(0);
             cur = mv12a(mvv, cc, Hh[k >> 2]);
           }

@@ -241,6 +241,42 @@ __device__ __forceinline__ void ld12s(double (&c)[12], const double* p) {  // a 
 #pragma unroll
   for (int i = 0; i < 12; ++i) c[i] = p[mo(i)];
 }
+// The same column as 12 separate ds_read_b64, issued without waiting: the compiler pairs ld12s's
+// loads into ds_read2_b64, which moves 16 B per lane in 8 LDS-array cycles against 2 x 2 for two
+// ds_read_b64.  The compiler does not track these loads: the values are valid only after
+// lds_wait<n>(c), n = the number of LDS instructions issued after them that may stay in flight
+// (LDS returns in order; lgkmcnt holds at most 15).
+__device__ __forceinline__ unsigned lds_off(const double* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) double*)p;
+}
+__device__ __forceinline__ void ldcol(double (&c)[12], const double* p) {
+  static_assert(mo(11) * 8 == 1072 && mo(4) * 8 == 400, "column offsets below");
+  const unsigned ad = lds_off(p);
+  asm volatile(
+      "ds_read_b64 %0, %12\n\t"
+      "ds_read_b64 %1, %12 offset:96\n\t"
+      "ds_read_b64 %2, %12 offset:192\n\t"
+      "ds_read_b64 %3, %12 offset:288\n\t"
+      "ds_read_b64 %4, %12 offset:400\n\t"
+      "ds_read_b64 %5, %12 offset:496\n\t"
+      "ds_read_b64 %6, %12 offset:592\n\t"
+      "ds_read_b64 %7, %12 offset:688\n\t"
+      "ds_read_b64 %8, %12 offset:784\n\t"
+      "ds_read_b64 %9, %12 offset:880\n\t"
+      "ds_read_b64 %10, %12 offset:976\n\t"
+      "ds_read_b64 %11, %12 offset:1072"
+      : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3]), "=&v"(c[4]), "=&v"(c[5]), "=&v"(c[6]),
+        "=&v"(c[7]), "=&v"(c[8]), "=&v"(c[9]), "=&v"(c[10]), "=&v"(c[11])
+      : "v"(ad));
+}
+template <int CNT>
+__device__ __forceinline__ void lds_wait(double (&c)[12]) {
+  static_assert(CNT >= 0 && CNT <= 15, "lgkmcnt range");
+  asm volatile("s_waitcnt lgkmcnt(%12)"
+               : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]),
+                 "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+               : "n"(CNT));
+}
 
 // The 12x12 discrete A = I + A_c dt (calculate_A_mat_c + state_space_discretization,
 // ConvexMpc.cpp:110-156) restricted to states 0..11: off-diagonals (0,6)=cy dt, (0,7)=sy dt,
