@@ -19,4 +19,5 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "scale_ker
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "scale_kernel|wave_kernel" --output-format csv \
   -d "$OUT/pmc/write" -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu "$@" > /dev/null 2> "$OUT/rocprof_write.err"
 tools/iter_cost.sh "$OUT/iter" > "$OUT/iter_cost.txt" 2>&1
+bash tools/pmc_lds.sh "$OUT/lds" > "$OUT/lds_cost.txt" 2>&1
 echo done
