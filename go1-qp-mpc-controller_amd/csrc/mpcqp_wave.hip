@@ -145,18 +145,19 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
           gen_col<N, BPT, true>(sm, p, A, dtm, j0, jb, [&](int jj, int b, int, double hv) __attribute__((always_inline)) {
             hc[12 * jj + b] = hv;
           });
+        // six independent max chains (a max is exact, so the grouping does not change the result)
+        double m6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int jj = 0; jj < BPT; ++jj) {
           const int j = jb + jj;
           if (j < N) {
             const double* dj = sm.D + ND * j;
 #pragma unroll
-            for (int b = 0; b < 12; ++b) {
-              if (b & 1) mx1 = fmax(mx1, dj[b] * dabs(hc[12 * jj + b]));
-              else mx0 = fmax(mx0, dj[b] * dabs(hc[12 * jj + b]));
-            }
+            for (int b = 0; b < 12; ++b) m6[b % 6] = fmax(m6[b % 6], dj[b] * dabs(hc[12 * jj + b]));
           }
         }
+        mx0 = fmax(fmax(m6[0], m6[2]), m6[4]);
+        mx1 = fmax(fmax(m6[1], m6[3]), m6[5]);
       } else {
         gen_col<N, BPT, false>(sm, p, A, dtm, j0, jb, [&](int, int b, int ri, double hv) __attribute__((always_inline)) {
           if (b & 1) mx1 = fmax(mx1, sm.D[ri] * dabs(hv));

@@ -310,6 +310,42 @@ __global__ __launch_bounds__(64) void chain_pf5_kernel(double* out, long long* c
   out[blockIdx.x * 64 + t] = cur;
   if (t == 0) cyc[blockIdx.x] = c1 - c0;
 }
+// chain_pf4 with only DPP row 0 loading (the chain runs in row 0; other rows idle)
+__global__ __launch_bounds__(64) void chain_row0_kernel(double* out, long long* cyc, int iters) {
+  extern __shared__ double lds[];
+  const int t = threadIdx.x, idx = t & 15;
+  for (int e = t; e < 9 * 144; e += 64) lds[e] = 1e-3 * ((e * 37) % 101) - 0.05;
+  __builtin_amdgcn_wave_barrier();
+  double cur = 0.5 + 0.01 * t;
+  const double ak = 0.125 * t;
+  const double* base = lds + 12 * (idx % 12);
+  double cn[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) cn[i] = base[i];
+  const long long c0 = __builtin_readcyclecounter();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      double c[12];
+#pragma unroll
+      for (int i = 0; i < 12; ++i) c[i] = cn[i];
+      if (t < 16) {
+        const double2* p = reinterpret_cast<const double2*>(base + 144 * ((k + 1) % 9));
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const double2 v = p[i];
+          cn[2 * i] = v.x;
+          cn[2 * i + 1] = v.y;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      cur = mv12i(cur, c, -ak);
+    }
+  }
+  const long long c1 = __builtin_readcyclecounter();
+  out[blockIdx.x * 64 + t] = cur;
+  if (t == 0) cyc[blockIdx.x] = c1 - c0;
+}
 // rows split the 12-term dot product: x rotated per row, 3 DPP FMAs, cross-row all-reduce
 __device__ __forceinline__ double rot_row(double x, int q) {  // row q lanes a <- lanes a + 4q
   const double r12 = __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x12C, 0xF, 0xF, false),
@@ -535,6 +571,7 @@ int main() {
     for (int w : W) run("chain_reg3", chain_reg3_kernel, w, 200, 9);
     for (int w : W) run("chain_pf4", chain_pf4_kernel, w, 200, 9);
     for (int w : W) run("chain_pf5", chain_pf5_kernel<0>, w, 200, 9);
+    for (int w : W) run("chain_row0", chain_row0_kernel, w, 200, 9);
     for (int w : W) run("chain_pf5_hand", chain_pf5_kernel<1>, w, 200, 9);
     return 0;
   }
