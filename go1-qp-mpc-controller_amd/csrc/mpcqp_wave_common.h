@@ -416,11 +416,16 @@ __device__ __forceinline__ double bcast_group(double x) {
 // code without EXEC writes, so the DPP source hazard needs 2 wait states, not 5.
 template <int L>
 __device__ __forceinline__ double rbcast(double x, double one) {
+#ifdef MPCQP_RBCAST_FMA
   double acc = 0.0;
   asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
       : "+v"(acc)
       : "v"(x), "v"(one), "i"(L));
   return acc;
+#else
+  (void)one;  // one v_mov_b64_dpp; the compiler sees it and inserts the DPP wait states itself
+  return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + L, 0xF, 0xF, false);
+#endif
 }
 // 1 / d: hardware reciprocal + two Newton steps (correct to the last bit or one ulp; the pivots of
 // an SPD matrix are positive and normal)
@@ -443,8 +448,9 @@ __device__ __forceinline__ void gj_inverse12(mf4& g) {
     const double pinv = recip(piv);
     const double rs = rowp * pinv;
     const bool jp = j == p;
+    // register 3 holds the pad rows 12-15: identity, zero in every pivot column, never changes
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < 3; ++v) {
       const double col = rbcast<p>(g[v], one);  // G[4v + grp][p]
       const double upd = jp ? -col * pinv : g[v] - col * rs;
       if (v == vp) g[v] = (grp == gp) ? (jp ? pinv : rs) : upd;  // row p
@@ -492,13 +498,16 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
     // G = R' + B'(P B): P B needs only B's rows 6-11 (K-blocks 1, 2); B' P B likewise
     const mf4 PB = mfma_chain<1, 3>(P, Bk, zero);
     G = mfma_chain<1, 3>(Bk, PB, G);
+    // the products that do not need G^-1 go to the matrix cores before the (VALU) inverse, so
+    // they run under it (step 0 computes them for nothing)
+    const mf4 PA = mfma_chain<0, 3>(P, Ad, zero);   // P A
+    const mf4 Fm = mfma_chain<1, 3>(Bk, PA, zero);  // F = B' P A
+    const mf4 Pq = mfma_chain<0, 3>(Ad, PA, cQ);    // cQ + A'P A
     gj_inverse12(G);
     if (j < 12)
 #pragma unroll
       for (int v = 0; v < 3; ++v) F.Gi[k][mo(4 * v + grp) + j] = G[v];
     if (k >= 1) {
-      const mf4 PA = mfma_chain<0, 3>(P, Ad, zero);         // P A
-      const mf4 Fm = mfma_chain<1, 3>(Bk, PA, zero);        // F = B' P A
       const mf4 K = mfma_chain<0, 3>(G, Fm, zero);          // K = G^-1 F
       if (j < 12)
 #pragma unroll
@@ -515,7 +524,7 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
       mf4 nF;
 #pragma unroll
       for (int v = 0; v < 4; ++v) nF[v] = -Fm[v];
-      P = mfma_chain<0, 3>(nF, K, mfma_chain<0, 3>(Ad, PA, cQ));  // cQ + A'PA - F'K
+      P = mfma_chain<0, 3>(nF, K, Pq);  // cQ + A'PA - F'K
     }
   }
   wave_sync();
