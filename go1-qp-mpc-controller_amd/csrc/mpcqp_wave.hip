@@ -621,7 +621,20 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       // LDS operands are loaded one phase ahead of their use; sched_barrier keeps the scheduler from
       // sinking a prefetch back down to its consumer (counted lgkmcnt waits then cover only it).
       double W[R], AKw[R], SMv[R], G[R], Hh[R], XS[R], tt[R];
-      double cA[R][12], cB[R][12], cw[R][3];
+      // Up to three rounds every phase's rows of all rounds are loaded one phase ahead (48 R VGPRs);
+      // beyond, each phase streams its rounds through two 12-double buffers.
+      constexpr bool PF = R <= 3;
+      double cA[PF ? R : 1][12], cB[PF ? R : 1][12], cw[PF ? R : 1][3];
+      // stream the rounds of a parallel phase: load(r, c) fills c with round r's rows, use(r, c)
+      auto pipe = [&](auto load, auto use) __attribute__((always_inline)) {
+        double c0[12], c1[12];
+        load(0, c0);
+        sfor<0, R>([&](auto RR) {
+          constexpr int r = decltype(RR)::value;
+          if constexpr (r + 1 < R) load(r + 1, (r & 1) ? c0 : c1);
+          use(r, (r & 1) ? c1 : c0);
+        });
+      };
       int kc[R], kk[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -632,8 +645,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         kk[r] = max(kc[r] - 1, 0);  // slot of K_k (k >= 1)
       }
       double cn[12];
+      if constexpr (PF) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) ldcol(cA[r], &F.K[kk[r]][idx]);
+        for (int r = 0; r < R; ++r) ldcol(cA[r], &F.K[kk[r]][idx]);
+      }
       // The chains load Acl one ROUND at a time: DPP row q takes the matrix of step 4 rr + gray(q) of
       // round rr, the step that row computes (every chain step runs in the row of its step), so one
       // 12-double load per lane serves four chain steps.
@@ -642,15 +657,21 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       if constexpr (N >= 3) ldcol(cn, &F.Acl[aslot((N - 2) >> 2)][idx]);
       __builtin_amdgcn_sched_barrier(0);
       // a_k = K_k' w_k (k >= 1)
+      if constexpr (PF) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) lds_wait<N >= 3 ? 12 : 0>(cA[r]);
-      mv_rounds<R>(W, cA, AKw);
+        for (int r = 0; r < R; ++r) lds_wait<N >= 3 ? 12 : 0>(cA[r]);
+        mv_rounds<R>(W, cA, AKw);
 #pragma unroll
-      for (int r = 0; r < R; ++r) {  // for g_k: G_k^-1 rows and B_k' columns
-        ld12(cB[r], &F.Gi[kc[r]][mo(idx)]);
-        cw[r][0] = sm.Bw[kc[r]][0][idx];
-        cw[r][1] = sm.Bw[kc[r]][1][idx];
-        cw[r][2] = sm.Bw[kc[r]][2][idx];
+        for (int r = 0; r < R; ++r) {  // for g_k: G_k^-1 rows and B_k' columns
+          ld12(cB[r], &F.Gi[kc[r]][mo(idx)]);
+          cw[r][0] = sm.Bw[kc[r]][0][idx];
+          cw[r][1] = sm.Bw[kc[r]][1][idx];
+          cw[r][2] = sm.Bw[kc[r]][2][idx];
+        }
+      } else {
+        lds_wait<0>(cn);  // (the chain's first columns; the streamed loads below are compiler-tracked)
+        pipe([&](int r, double (&c)[12]) __attribute__((always_inline)) { ld12s(c, &F.K[kk[r]][idx]); },
+             [&](int r, const double (&c)[12]) __attribute__((always_inline)) { AKw[r] = mv12(W[r], c); });
       }
       __builtin_amdgcn_sched_barrier(0);
       if (tm_it) WV_MARK(41);
@@ -675,30 +696,40 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       }
       if (tm_it) WV_MARK(42);
       // g_k = G_k^-1 (w_k + B_k' s_{k+1})
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const double c6[6] = {cw[r][0], cw[r][1], cw[r][2], a == 0 ? dtm : 0.0, a == 1 ? dtm : 0.0,
-                              a == 2 ? dtm : 0.0};
-        tt[r] = W[r] + mv6(SMv[r], c6);
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) ld12(cA[r], &sm.Bw[kc[r]][av ? a : 2][0]);  // for h_k
-      __builtin_amdgcn_sched_barrier(0);
-      mv_rounds<R>(tt, cB, G);
+      auto ttr = [&](int r, double c0, double c1, double c2) __attribute__((always_inline)) {
+        const double c6[6] = {c0, c1, c2, a == 0 ? dtm : 0.0, a == 1 ? dtm : 0.0, a == 2 ? dtm : 0.0};
+        return W[r] + mv6(SMv[r], c6);
+      };
       // h_k = B_k g_k: rows 6-8 (leg-2 lanes) B_w g, rows 9-11 (leg-3 lanes) dt/m times the sum of
       // the legs' matching force component, rows 0-5 zero
-      if constexpr (N >= 3) ld12(cn, &F.Acl[aslot(0)][mo(idx)]);
+      auto hhr = [&](int r, double hb) __attribute__((always_inline)) {
+        const double ls = dtm * legsum(G[r]);
+        return leg == 2 ? hb : (leg == 3 ? ls : 0.0);
+      };
+      if constexpr (PF) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) ld12(cB[r], &F.K[kk[r]][mo(idx)]);  // for u_k
-      __builtin_amdgcn_sched_barrier(0);
-      {
+        for (int r = 0; r < R; ++r) tt[r] = ttr(r, cw[r][0], cw[r][1], cw[r][2]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) ld12(cA[r], &sm.Bw[kc[r]][av ? a : 2][0]);  // for h_k
+        __builtin_amdgcn_sched_barrier(0);
+        mv_rounds<R>(tt, cB, G);
+        if constexpr (N >= 3) ld12(cn, &F.Acl[aslot(0)][mo(idx)]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) ld12(cB[r], &F.K[kk[r]][mo(idx)]);  // for u_k
+        __builtin_amdgcn_sched_barrier(0);
         double hb[R];
         mv_rounds<R>(G, cA, hb);
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const double ls = dtm * legsum(G[r]);
-          Hh[r] = leg == 2 ? hb[r] : (leg == 3 ? ls : 0.0);
-        }
+        for (int r = 0; r < R; ++r) Hh[r] = hhr(r, hb[r]);
+      } else {
+        pipe([&](int r, double (&c)[12]) __attribute__((always_inline)) { ld12(c, &F.Gi[kc[r]][mo(idx)]); },
+             [&](int r, const double (&c)[12]) __attribute__((always_inline)) {
+               tt[r] = ttr(r, sm.Bw[kc[r]][0][idx], sm.Bw[kc[r]][1][idx], sm.Bw[kc[r]][2][idx]);
+               G[r] = mv12(tt[r], c);
+             });
+        pipe([&](int r, double (&c)[12]) __attribute__((always_inline)) { ld12(c, &sm.Bw[kc[r]][av ? a : 2][0]); },
+             [&](int r, const double (&c)[12]) __attribute__((always_inline)) { Hh[r] = hhr(r, mv12(G[r], c)); });
+        if constexpr (N >= 3) ld12(cn, &F.Acl[aslot(0)][mo(idx)]);
       }
       if (tm_it) WV_MARK(43);
       {  // forward chain: x_1 = h_0; x_{k+1} = Acl_k x_k + h_k; XS (row of k) = x_k
@@ -721,11 +752,14 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       }
       if (tm_it) WV_MARK(44);
       // u_k = g_k - K_k x_k (x_0 = 0)
-      {
+      if constexpr (PF) {
         double kx[R];
         mv_rounds<R>(XS, cB, kx);
 #pragma unroll
         for (int r = 0; r < R; ++r) U[r] = G[r] - kx[r];
+      } else {
+        pipe([&](int r, double (&c)[12]) __attribute__((always_inline)) { ld12(c, &F.K[kk[r]][mo(idx)]); },
+             [&](int r, const double (&c)[12]) __attribute__((always_inline)) { U[r] = G[r] - mv12(XS[r], c); });
       }
 #ifdef MPCQP_DBG
       for (int r = 0; r < R; ++r)
