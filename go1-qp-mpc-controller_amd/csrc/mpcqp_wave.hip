@@ -661,13 +661,6 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 #pragma unroll
         for (int r = 0; r < R; ++r) lds_wait<N >= 3 ? 12 : 0>(cA[r]);
         mv_rounds<R>(W, cA, AKw);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {  // for g_k: G_k^-1 rows and B_k' columns
-          ld12(cB[r], &F.Gi[kc[r]][mo(idx)]);
-          cw[r][0] = sm.Bw[kc[r]][0][idx];
-          cw[r][1] = sm.Bw[kc[r]][1][idx];
-          cw[r][2] = sm.Bw[kc[r]][2][idx];
-        }
       } else {
         lds_wait<0>(cn);  // (the chain's first columns; the streamed loads below are compiler-tracked)
         pipe([&](int r, double (&c)[12]) __attribute__((always_inline)) { ld12s(c, &F.K[kk[r]][idx]); },
@@ -675,6 +668,21 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       }
       __builtin_amdgcn_sched_barrier(0);
       if (tm_it) WV_MARK(41);
+      // g_k's G_k^-1 rows and B_k' columns: issued when the backward chain enters its last round
+      // (three steps before their use), so they do not hold registers through the whole chain
+      auto load_g = [&]() __attribute__((always_inline)) {
+        if constexpr (PF) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            ld12(cB[r], &F.Gi[kc[r]][mo(idx)]);
+            cw[r][0] = sm.Bw[kc[r]][0][idx];
+            cw[r][1] = sm.Bw[kc[r]][1][idx];
+            cw[r][2] = sm.Bw[kc[r]][2][idx];
+          }
+        }
+      };
+      constexpr int KG = N - 2 >= 3 ? 3 : N - 2;  // the backward chain's step that issues them
+      if constexpr (KG < 1) load_g();
       {  // backward chain: s_{N-1} = -a_{N-1}; s_k = Acl_k' s_{k+1} - a_k; SMv (row of k) = s_{k+1}
         double cur = -AKw[(N - 1) >> 2];
         double cc[12];
@@ -689,6 +697,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
               for (int e = 0; e < 12; ++e) cc[e] = cn[e];
               if constexpr (k >= 4) ldcol(cn, &F.Acl[aslot((k >> 2) - 1)][idx]);  // the next round's columns
             }
+            if constexpr (k == KG) load_g();
             __builtin_amdgcn_sched_barrier(0);
             cur = mv12a(mvv, cc, -AKw[k >> 2]);
           }
@@ -714,8 +723,6 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         __builtin_amdgcn_sched_barrier(0);
         mv_rounds<R>(tt, cB, G);
         if constexpr (N >= 3) ld12(cn, &F.Acl[aslot(0)][mo(idx)]);
-#pragma unroll
-        for (int r = 0; r < R; ++r) ld12(cB[r], &F.K[kk[r]][mo(idx)]);  // for u_k
         __builtin_amdgcn_sched_barrier(0);
         double hb[R];
         mv_rounds<R>(G, cA, hb);
@@ -732,6 +739,15 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         if constexpr (N >= 3) ld12(cn, &F.Acl[aslot(0)][mo(idx)]);
       }
       if (tm_it) WV_MARK(43);
+      // u_k's K_k rows: issued three steps before the forward chain ends
+      auto load_u = [&]() __attribute__((always_inline)) {
+        if constexpr (PF) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) ld12(cB[r], &F.K[kk[r]][mo(idx)]);
+        }
+      };
+      constexpr int KU = N - 2 >= 1 ? (N - 4 > 1 ? N - 4 : 1) : 0;  // three steps before the end
+      if constexpr (KU < 1) load_u();
       {  // forward chain: x_1 = h_0; x_{k+1} = Acl_k x_k + h_k; XS (row of k) = x_k
         double cur = Hh[0];
         double cc[12];
@@ -745,6 +761,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
               for (int e = 0; e < 12; ++e) cc[e] = cn[e];
               if constexpr (4 * ((k >> 2) + 1) <= N - 2) ld12(cn, &F.Acl[aslot((k >> 2) + 1)][mo(idx)]);
             }
+            if constexpr (k == KU) load_u();
             __builtin_amdgcn_sched_barrier(0);
             cur = mv12a(mvv, cc, Hh[k >> 2]);
           }
