@@ -681,7 +681,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
           }
         }
       };
-      constexpr int KG = N - 2 >= 3 ? 3 : N - 2;  // the backward chain's step that issues them
+      constexpr int KG = N - 2 >= 2 ? 2 : N - 2;  // the backward chain's step that issues them
       if constexpr (KG < 1) load_g();
       {  // backward chain: s_{N-1} = -a_{N-1}; s_k = Acl_k' s_{k+1} - a_k; SMv (row of k) = s_{k+1}
         double cur = -AKw[(N - 1) >> 2];
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
           for (int r = 0; r < R; ++r) ld12(cB[r], &F.K[kk[r]][mo(idx)]);
         }
       };
-      constexpr int KU = N - 2 >= 1 ? (N - 4 > 1 ? N - 4 : 1) : 0;  // three steps before the end
+      constexpr int KU = N - 2 >= 1 ? (N - 3 > 1 ? N - 3 : 1) : 0;  // two steps before the end
       if constexpr (KU < 1) load_u();
       {  // forward chain: x_1 = h_0; x_{k+1} = Acl_k x_k + h_k; XS (row of k) = x_k
         double cur = Hh[0];
