@@ -73,7 +73,7 @@ def main():
                     help="instances timed on the CPU oracle (4096 x ~2.3 ms = ~10 s of CPU work)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--solver", default="auto", choices=["auto", "dense", "riccati", "wave", "mw"],
+    ap.add_argument("--solver", default="auto", choices=["auto", "dense", "riccati", "wave", "mw", "dx"],
                     help="linear-system path (mpcqp_debug_set_solver); auto = the library default")
     args = ap.parse_args()
 
@@ -94,7 +94,7 @@ def main():
     config_id = 1 if (args.gait == "trot" and not args.mixed_mu) else 4
     params = mpcqp.default_params(N)
     solver = mpcqp.MpcQpSolver(params, device=local_rank)
-    path = {"auto": 0, "dense": 1, "riccati": 2, "wave": 3, "mw": 4}[args.solver]
+    path = {"auto": 0, "dense": 1, "riccati": 2, "wave": 3, "mw": 4, "dx": 5}[args.solver]
     if path:
         solver.set_solver(path)
     solver.reserve(B)
@@ -181,7 +181,8 @@ def main():
         eff = path or 3
         kernel_name = {1: f"mpcqp::solve_kernel<{N}>", 2: f"mpcqp::ric::ric_solve_kernel<{N}>",
                        3: f"mpcqp::wv::scale_kernel<{N}> + mpcqp::wv::wave_kernel<{N}>",
-                       4: f"mpcqp::wv::scale_kernel<{N}> + mpcqp::mw::mw_kernel<{N}>"}[eff]
+                       4: f"mpcqp::wv::scale_kernel<{N}> + mpcqp::mw::mw_kernel<{N}>",
+                       5: f"mpcqp::wv::scale_kernel<{N}> + mpcqp::dx::dx_kernel<{N}>"}[eff]
         traffic = load_traffic(key, kernel_name)
         out = {
             "metric": METRIC,

@@ -22,7 +22,7 @@ struct mpcqp_handle {
   double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
   size_t work_per = 0;       // doubles per instance the workspace was sized for
-  int path = 0;              // 0 auto, 1 dense K^-1, 2 Riccati workgroup, 3 Riccati wave, 4 wave per round (mpcqp_debug_set_solver)
+  int path = 0;              // 0 auto, 1 dense K^-1, 2 Riccati workgroup, 3 Riccati wave, 4 wave per round, 5 register K^-1 (mpcqp_debug_set_solver)
   // host wrapper staging
   double* d_recs = nullptr;
   mpcqp_result* d_res = nullptr;
@@ -90,6 +90,7 @@ hipError_t occupancy_for(const mpcqp_handle* h, int* per_cu) {
     case 1: return mpcqp::occupancy_any(h->p.horizon, per_cu);
     case 2: return mpcqp::occupancy_riccati_any(h->p.horizon, per_cu);
     case 3: return mpcqp::occupancy_wave_any(h->p.horizon, per_cu);
+    case 5: return mpcqp::occupancy_dx_any(h->p.horizon, per_cu);
     default: return mpcqp::occupancy_mw_any(h->p.horizon, per_cu);
   }
 }
@@ -213,6 +214,7 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
     case 1: e = mpcqp::launch_solve_any(a); break;
     case 2: e = mpcqp::launch_riccati_any(a); break;
     case 3: e = mpcqp::launch_wave_any(a); break;
+    case 5: e = mpcqp::launch_dx_any(a); break;
     default: e = mpcqp::launch_mw_any(a); break;
   }
   if (e != hipSuccess) return set_hip_error(h, e, "solve_kernel launch");
@@ -410,8 +412,8 @@ int32_t mpcqp_solve_threads(int32_t horizon) {
 }
 
 int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
-  if (!h || path < 0 || path > 4) return MPCQP_ERR_INVALID_ARG;
-  if (path == 1 && h->p.horizon > mpcqp::DENSE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
+  if (!h || path < 0 || path > 5) return MPCQP_ERR_INVALID_ARG;
+  if ((path == 1 || path == 5) && h->p.horizon > mpcqp::DENSE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
   if (path >= 3 && h->p.horizon > mpcqp::WAVE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
   DeviceGuard dg(h->device);
   hipError_t e = dg.err;
@@ -431,6 +433,11 @@ int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
 int32_t mpcqp_debug_wave_selftest(double* d_out, void* stream) {
   if (!d_out) return MPCQP_ERR_INVALID_ARG;
   return mpcqp::wave_selftest(d_out, stream) == hipSuccess ? MPCQP_OK : MPCQP_ERR_HIP;
+}
+
+int32_t mpcqp_debug_dx_selftest(double* d_out, void* stream) {
+  if (!d_out) return MPCQP_ERR_INVALID_ARG;
+  return mpcqp::dx_selftest(d_out, stream) == hipSuccess ? MPCQP_OK : MPCQP_ERR_HIP;
 }
 
 }  // extern "C"

@@ -45,6 +45,10 @@ hipError_t launch_scale_any(const LaunchArgs& a);  // scale_kernel alone (the im
 hipError_t launch_mw_any(const LaunchArgs& a);
 hipError_t occupancy_mw_any(int horizon, int* blocks);
 constexpr int WAVE_MAX_HORIZON = 20;
+// Register-resident K^-1 path (mpcqp_dx.hip): scale_kernel + dx_kernel, horizons 1..DENSE_MAX_HORIZON
+hipError_t launch_dx_any(const LaunchArgs& a);
+hipError_t occupancy_dx_any(int horizon, int* blocks);
+hipError_t dx_selftest(double* d_out, void* stream);
 // doubles per robot of the warm-start slot (mpcqp_wave.hip WarmLayout)
 __host__ __device__ constexpr int warm_state_doubles(int N) {
   return 4 + 3 * 12 * N + 5 * 20 * N + ((12 * N + 63) / 64) * 12 * N;

@@ -603,8 +603,9 @@ __device__ __forceinline__ void block_sum_max(double& sv, double& qv, double (*r
 //   block j >  k:  H_jk e_a = B_j' S_j A^{j-k} y   = B_j' S_j (y + (j-k) Ac y)
 // where only rows 6-11 of the 12-vector inside B_j' matter).  Blocks jb .. jb+NB-1 (< N) only;
 // sink(jj, b, ri, hv) receives entry ri = 12 j + b of block j = jb + jj, jj and b compile-time.
-template <int N, int NB, bool UNROLL, class Sink>
-__device__ __forceinline__ void gen_col(const ScaleSmem<N>& sm, const mpcqp_params& p, const Adisc& A, double dtm,
+// SM: any LDS image with the B_w rows (Bw[N][3][ND]).
+template <int N, int NB, bool UNROLL, class SM, class Sink>
+__device__ __forceinline__ void gen_col(const SM& sm, const mpcqp_params& p, const Adisc& A, double dtm,
                                         int c, int jb, Sink&& sink) {
   const double dt = A.dt;
   const int k = c / ND, a2 = c % ND;

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(PKG_ROOT, "lib", "libmpcq
 STATE_DIM, NUM_LEG, NUM_DOF, CONSTRAINT_DIM = 13, 4, 12, 20
 MAX_HORIZON = 20
 DENSE_MAX_HORIZON = 10  # the dense K^-1 path (debug selection) serves horizons up to this
-SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI, SOLVER_WAVE, SOLVER_WAVE_MW = 0, 1, 2, 3, 4
+SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI, SOLVER_WAVE, SOLVER_WAVE_MW, SOLVER_DX = 0, 1, 2, 3, 4, 5
 OSQP_INFTY = 1e30
 
 # record layout (include/mpcqp.h MPCQP_REC_*)
@@ -99,7 +99,7 @@ EXPORTED = [
     "mpcqp_solve_batch_device", "mpcqp_solve_batch_host", "mpcqp_build_qp_device",
     "mpcqp_status_str", "mpcqp_error_str", "mpcqp_last_error",
     "mpcqp_debug_solve_trace_device", "mpcqp_abi_sizes", "mpcqp_handle_slots", "mpcqp_solve_threads",
-    "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_joint_torques_device",
+    "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_debug_dx_selftest", "mpcqp_joint_torques_device",
     "mpcqp_warm_state_size", "mpcqp_solve_batch_warm_device",
     "mpcqp_balance_default_params", "mpcqp_balance_solve_device", "mpcqp_assemble_records_device",
     "mpcqp_balance_solve_host",
@@ -155,6 +155,8 @@ def load():
     L.mpcqp_debug_set_solver.restype = i32
     L.mpcqp_debug_wave_selftest.argtypes = [vp, vp]
     L.mpcqp_debug_wave_selftest.restype = i32
+    L.mpcqp_debug_dx_selftest.argtypes = [vp, vp]
+    L.mpcqp_debug_dx_selftest.restype = i32
     L.mpcqp_joint_torques_device.argtypes = [vp, vp, i32, vp, vp, vp]
     L.mpcqp_joint_torques_device.restype = i32
     L.mpcqp_warm_state_size.argtypes = [i32]
