@@ -41,7 +41,7 @@
 // free of the Riccati chains, is latency-bound behind its per-iteration barrier and the
 // permlane / DPP hand-offs at one or two waves per SIMD (K's row takes 120 of the 256 VGPRs).
 // Debug build: -DDXE_DUMP writes K, K^-1, D, E, c, rho of the first factorization into
-// `solution` (tools/dx_dump.py); -DMPCQP_DX_WPE=1 sizes the registers for one wave per SIMD.
+// `solution` (tools/dx_dump.py); -DMPCQP_DX_WPE=2 sizes the registers for two waves per SIMD.
 #include "mpcqp_wave_common.h"
 
 namespace mpcqp {
@@ -184,7 +184,11 @@ __device__ __forceinline__ void block_red(double (&v)[K], double (*red)[NWV][16]
 
 template <int N>
 #ifndef MPCQP_DX_WPE
-#define MPCQP_DX_WPE 2  // waves per SIMD the register budget is sized for
+// waves per SIMD the register budget is sized for: at 2 (256 VGPRs) the compiler spills ~170
+// VGPRs to scratch and the N = 6 build failed parity (N = 1-5, 7-10 passed); at 1 (VGPRs + AGPRs
+// up to 512) nothing spills, all horizons pass, and the per-iteration cost is the same
+// (11.8 vs 12.0 us per 4096-robot batch, tools/dx_timing.py)
+#define MPCQP_DX_WPE 1
 #endif
 __global__ __launch_bounds__(DCfg<N>::NTH, MPCQP_DX_WPE) void dx_kernel(const double* __restrict__ recs, int batch,
                                                               mpcqp_result* __restrict__ results,
