@@ -829,6 +829,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       const double pxt = (RHS[r] - sigma * xt) - kd;
       PXO[r] = PX[r];
       PX[r] = alpha * pxt + (1.0 - alpha) * PX[r];
+      // next right-hand side sigma x - q~ + A~'(rho z - y), here so that it interleaves with the other
+      // rounds' updates (recomputed below when adapt_rho changes rho)
+      const double at = quad_at(rho * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
+      RHS[r] = (sigma * X[r] - Qv[r]) + at;
     }
 
     if (tm_it) WV_MARK(46);
@@ -1001,14 +1005,13 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         }
         rinv = 1. / rho;
         need_factor = true;
-      }
-    }
-    // ---- next right-hand side: sigma x - q~ + A~'(rho z - y) ----
+        // the right-hand side with the new rho vector
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      // (padding lanes and steps past N compute values nothing reads unmasked)
-      const double at = quad_at(rho * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
-      RHS[r] = (sigma * X[r] - Qv[r]) + at;
+        for (int r = 0; r < R; ++r) {
+          const double at = quad_at(rho * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
+          RHS[r] = (sigma * X[r] - Qv[r]) + at;
+        }
+      }
     }
     if (tm_it) WV_MARK(47);
   }
