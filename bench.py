@@ -2,17 +2,27 @@
 """Benchmark: batched Go1 convex-MPC QP solves/sec on MI355X (BASELINE.json metric).
 
 One step = one pass of the hot path over one batch of synthetic robot states resident in HBM:
-condensation + Ruiz scaling + KKT inverse + OSQP-0.6 ADMM + extraction (solve_kernel), and for
-N > 1 the RCCL all-gather of the solved forces over xGMI (north_star, config C3).
+scale_kernel (OSQP scale_data on the condensed Hessian's closed-form columns) + wave_kernel
+(Riccati KKT factorization on MFMA, OSQP-0.6 ADMM, extraction), and for N > 1 ranks the RCCL
+all-gather of the solved forces over xGMI (north_star, config C3).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--horizon 10]
-  (N > 1: launched by torch.distributed.run, one rank per GPU)
 
-Prints ONE JSON line on rank 0.
+--gpus N > 1 without a torch.distributed environment: this process starts
+`python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child (it never touches the
+GPU itself) and exits with the child's code.  Every rank takes the contiguous shard
+shard_range(N*B, N, rank) of ONE seeded global batch of N*B robots (weak scaling: B robots per GPU;
+C3 = --gpus 8 --batch 8192), solves it and all-gathers u0 with mpcqp.distributed.allgather_forces.
+Rank 0 checks the world size, checks the gathered forces against the CPU oracle on a 4096-robot
+sample spread over every shard, and prints ONE JSON line.
+
+At N = 1 the line also carries the CPU baseline (the oracle on the host cores) and extra keys,
+each with its own parity sample: e2e (host buffers in and out through mpcqp_solve_batch_host),
+assemble_e2e (raw robot-state rows -> on-device assembly -> solve), c4 (horizon 20), c5 (mixed
+gait, random mu, 8192 robots), warm_tick (closed-loop warm-started ticks).
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -24,6 +34,7 @@ sys.path.insert(0, os.path.join(REPO, "go1-qp-mpc-controller_amd"))
 
 METRIC = "MPC QP solves/sec (horizon=10, 12 GRF vars) at 1/2/4/8 MI355X vs CPU OSQP"
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, spec
+PARITY_SAMPLE = 4096
 
 
 def algorithmic_flops(N, iters, rho_updates):
@@ -60,12 +71,12 @@ def load_traffic(config_key, kernel):
     return e.get("hbm_bytes_per_launch")
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="robots per GPU (configs[1]: 4096)")
+    ap.add_argument("--batch", type=int, default=4096, help="robots per GPU (configs[1]: 4096; C3: 8192)")
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--gait", default="trot", choices=["trot", "stance", "mixed"])
     ap.add_argument("--mixed-mu", action="store_true")
@@ -73,153 +84,384 @@ def main():
                     help="instances timed on the CPU oracle (4096 x ~2.3 ms = ~10 s of CPU work)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--solver", default="auto", choices=["auto", "dense", "riccati", "wave", "mw", "dx"],
-                    help="linear-system path (mpcqp_debug_set_solver); auto = the library default")
-    args = ap.parse_args()
+    ap.add_argument("--no-extras", action="store_true", help="skip the e2e / c4 / c5 / warm_tick keys")
+    ap.add_argument("--cpu-stub", action="store_true",
+                    help="TEST ONLY: gloo backend on the CPU, a deterministic stub in place of the device "
+                         "solve (exercises the launcher, sharding and all-gather without a GPU)")
+    return ap.parse_args(argv)
 
+
+def oracle_module():
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle  # checker / CPU-baseline leg only (test infrastructure)
+    pyoracle.build()
+    return pyoracle
+
+
+def parity_of(got, ref):
+    """u0 relative error (SURVEY §8(c) gate 1e-4), status and iteration equality."""
+    err = np.max(np.abs(got["u0"] - ref["u0"]), axis=1) / np.maximum(np.max(np.abs(ref["u0"]), axis=1), 1.0)
+    return {"max_rel_err_u0": float(np.max(err)) if err.size else 0.0, "instances": int(len(ref)),
+            "status_equal": bool(np.all(got["status"] == ref["status"])),
+            "iters_equal": bool(np.all(got["iters"] == ref["iters"])),
+            "iters_equal_frac": float(np.mean(got["iters"] == ref["iters"])) if len(ref) else 1.0}
+
+
+def workload(N, total, gait, mixed_mu):
+    """One seeded synthetic global batch; every rank builds the same one."""
+    import mpcqp
+    config_id = 1 if (gait == "trot" and not mixed_mu) else 4
+    states = mpcqp.synthetic_go1(total, seed=config_id * 1000, gait=gait, mixed_mu=mixed_mu)
+    return states, mpcqp.assemble_compute_grf(states, N)
+
+
+def stub_results(recs):
+    """--cpu-stub: a deterministic per-robot stand-in for the solve (u0 from the record bytes)."""
+    import mpcqp
+    res = np.zeros(recs.shape[0], dtype=mpcqp.RESULT_DTYPE)
+    res["u0"] = recs[:, :12] * 3.0 + recs[:, 44:56]
+    res["status"] = 1
+    res["iters"] = 25
+    return res
+
+
+def as_rows(res):
+    """mpcqp_result structured array -> [B, 30] float64 rows (bit copy) and back."""
+    return np.frombuffer(res.tobytes(), dtype=np.float64).reshape(len(res), -1)
+
+
+def run_rank(args):
     import torch
     import torch.distributed as dist
     import mpcqp
+    from mpcqp.distributed import allgather_forces, env_rank, shard_range
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
+    world, rank, local_rank = env_rank()
+    if args.cpu_stub:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+    ranks_seen = dist.get_world_size() if world > 1 else 1
+    if ranks_seen != args.gpus:
+        raise SystemExit(f"bench: {ranks_seen} ranks but --gpus {args.gpus}")
 
     N, B = args.horizon, args.batch
-    config_id = 1 if (args.gait == "trot" and not args.mixed_mu) else 4
-    params = mpcqp.default_params(N)
-    solver = mpcqp.MpcQpSolver(params, device=local_rank)
-    path = {"auto": 0, "dense": 1, "riccati": 2, "wave": 3, "mw": 4, "dx": 5}[args.solver]
-    if path:
-        solver.set_solver(path)
-    solver.reserve(B)
+    total = B * world
+    states, recs_global = workload(N, total, args.gait, args.mixed_mu)
+    b0, b1 = shard_range(total, world, rank)
+    recs_np = np.ascontiguousarray(recs_global[b0:b1])
+    Bl = b1 - b0
+    RD = mpcqp._lib.RESULT_DOUBLES
 
-    # synthetic Go1 states, seed = config*1000 + rank; records resident in HBM
-    states = mpcqp.synthetic_go1(B, seed=config_id * 1000 + rank, gait=args.gait, mixed_mu=args.mixed_mu)
-    recs_np = mpcqp.assemble_compute_grf(states, N)
-    d_rec = torch.from_numpy(recs_np).to(dev)
-    d_res = torch.zeros((B, mpcqp._lib.RESULT_DOUBLES), dtype=torch.float64, device=dev)
-    d_forces = d_res[:, :12]  # u0 (world-frame GRF of step 0), strided view
-    gathered = torch.empty((world * B, 12), dtype=torch.float64, device=dev) if world > 1 else None
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
+    params = None
+    solver = None
+    if args.cpu_stub:
+        stub = torch.from_numpy(as_rows(stub_results(recs_np)).copy())
+        d_res = torch.zeros((Bl, RD), dtype=torch.float64)
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        solver.solve_device(d_rec.data_ptr(), B, d_res.data_ptr(), 0, sptr)
-        if ev is not None:
-            ev[1].record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, d_forces.contiguous())
+        def solve():
+            d_res.copy_(stub)
+        sync = (lambda: None)
+        events = None
+    else:
+        params = mpcqp.default_params(N)
+        solver = mpcqp.MpcQpSolver(params, device=local_rank)
+        solver.reserve(Bl)
+        d_rec = torch.from_numpy(recs_np).to(dev)
+        d_res = torch.zeros((Bl, RD), dtype=torch.float64, device=dev)
+        stream = torch.cuda.current_stream(dev)
+
+        def solve():
+            solver.solve_device(d_rec.data_ptr(), Bl, d_res.data_ptr(), 0, stream.cuda_stream)
+
+        def sync():
+            torch.cuda.synchronize(dev)
+        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(args.steps)]
+
+    def step(k=None):
+        if events is not None and k is not None:
+            events[k][0].record(stream)
+        solve()
+        if events is not None and k is not None:
+            events[k][1].record(stream)
+        if world > 1:  # the production exchange: u0 of every robot on every rank
+            return allgather_forces(d_res[:, :12].contiguous(), total)
+        return None
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(events[k])
-    torch.cuda.synchronize(dev)
+        full = step(k)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else None
 
-    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE).copy()
-    flops = algorithmic_flops(N, res["iters"], res["rho_updates"])  # per launch (this rank's batch)
-    achieved_tflops = flops / (kern_ms * 1e-3) / 1e12
-    total_qp = world * B * args.steps
-    value = total_qp / elapsed
+    # whole results of every rank (outside the timed region) for the parity sample
+    if world > 1:
+        all_rows = allgather_forces(d_res, total).cpu().numpy()
+        u0_full = full.cpu().numpy()
+    else:
+        all_rows = d_res.cpu().numpy()
+        u0_full = all_rows[:, :12]
+    res_all = np.frombuffer(np.ascontiguousarray(all_rows).tobytes(), dtype=mpcqp.RESULT_DTYPE).copy()
+    local_res = res_all[b0:b1]
+    value = total * args.steps / elapsed
 
     out = None
     if rank == 0:
-        cpu = None
-        parity = None
-        if world == 1 and not args.no_cpu:
-            sys.path.insert(0, os.path.join(REPO, "oracle"))
-            import pyoracle  # CPU baseline leg only (test infrastructure)
-            pyoracle.build()
-            S = min(args.cpu_sample, B)
-            nthr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            op = pyoracle.default_params(N, q=list(params.q_weights), r=list(params.r_weights))
-            pyoracle.solve_batch(op, recs_np[:min(S, 64)], nthreads=nthr)  # warm
-            tc = time.perf_counter()
-            ref = pyoracle.solve_batch(op, recs_np[:S], nthreads=nthr)
-            tcpu = time.perf_counter() - tc
-            t1 = time.perf_counter()
-            pyoracle.solve_batch(op, recs_np[:min(S, 128)], nthreads=1)
-            t1 = (time.perf_counter() - t1) / min(S, 128)
-            cpu = {"value": S / tcpu, "unit": "QP/s", "cores": nthr, "kind": "port",
-                   "sample": f"first {S} instances of this workload (same seed) on oracle/mpc_oracle.c "
-                             f"(binary64 ConvexMpc + OSQP-0.6 restatement), {nthr} host threads; "
-                             f"single-thread {t1 * 1e6:.0f} us/QP",
-                   "single_thread_us_per_qp": t1 * 1e6}
-            err = np.max(np.abs(res["u0"][:S] - ref["u0"]), axis=1) / np.maximum(
-                np.max(np.abs(ref["u0"]), axis=1), 1.0)
-            parity = {"max_rel_err_u0": float(np.max(err)), "instances": int(S),
-                      "status_equal": bool(np.all(res["status"][:S] == ref["status"])),
-                      "iters_equal": bool(np.all(res["iters"][:S] == ref["iters"]))}
-        workload = (f"Go1 convex-MPC GRF QP, horizon {N} (n={12 * N}, m={20 * N}), {B} robots/GPU, "
-                    f"{args.gait} gait{', mu~U(0.3,0.9)' if args.mixed_mu else ''}; "
-                    f"cold-start OSQP-0.6 settings, adaptive-rho interval 25")
-        key = f"N{N}_B{B}_{args.gait}{'_mu' if args.mixed_mu else ''}"
-        eff = path or 3
-        kernel_name = {1: f"mpcqp::solve_kernel<{N}>", 2: f"mpcqp::ric::ric_solve_kernel<{N}>",
-                       3: f"mpcqp::wv::scale_kernel<{N}> + mpcqp::wv::wave_kernel<{N}>",
-                       4: f"mpcqp::wv::scale_kernel<{N}> + mpcqp::mw::mw_kernel<{N}>",
-                       5: f"mpcqp::wv::scale_kernel<{N}> + mpcqp::dx::dx_kernel<{N}>"}[eff]
-        traffic = load_traffic(key, kernel_name)
-        out = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "QP/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (seeded Go1 states per SURVEY §8(d); no dataset needed)",
-            "config": {"workload": workload, "batch_per_gpu": B, "global_batch": world * B,
-                       "horizon": N, "gait": args.gait, "parallelism": f"dp{world}",
-                       "collective": "RCCL all_gather of u0 per step" if world > 1 else "none"},
-            "roofline": {"bound": "valu_fp64", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS,
-                         "traffic": traffic,
-                         "kernel": kernel_name, "kernel_ms": kern_ms,
-                         "algorithmic_flop_per_launch": flops,
-                         "note": "binary64; the ADMM iterations (86% of the solve) run on the VALU "
-                                 "(v_fmac_f64 DPP mat-vecs) and bound it, the Riccati factorization "
-                                 "runs on v_mfma_f64_16x16x4f64; peak = FP64 vector spec (equal to "
-                                 "the FP64 MFMA peak on gfx950)"},
-            "cpu_baseline": cpu,
-            "parity": parity,
-            "stats": {"mean_iters": float(res["iters"].mean()), "max_iters": int(res["iters"].max()),
-                      "mean_rho_updates": float(res["rho_updates"].mean()),
-                      "solved_frac": float(np.mean(res["status"] == 1))},
-        }
-        print(json.dumps(out), flush=True)
-    solver.close()
+        out = {"metric": METRIC, "value": value, "unit": "QP/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic (seeded Go1 states per SURVEY §8(d); no dataset needed)"}
+        workload_s = (f"Go1 convex-MPC GRF QP, horizon {N} (n={12 * N}, m={20 * N}), {B} robots/GPU, "
+                      f"{args.gait} gait{', mu~U(0.3,0.9)' if args.mixed_mu else ''}; "
+                      f"cold-start OSQP-0.6 settings, adaptive-rho interval 25")
+        out["config"] = {"workload": workload_s, "batch_per_gpu": B, "global_batch": total, "horizon": N,
+                         "gait": args.gait, "parallelism": f"dp{world}", "ranks_seen": ranks_seen,
+                         "sharding": "contiguous shard_range of one seeded global batch per rank",
+                         "collective": "RCCL all_gather of u0 per step (mpcqp.distributed.allgather_forces)"
+                         if world > 1 else "none"}
+        gather_ok = bool(np.array_equal(u0_full, res_all["u0"])) if world > 1 else True
+        if args.cpu_stub:
+            exp = stub_results(recs_global)
+            out["parity"] = {"gather_exact": bool(np.array_equal(u0_full, exp["u0"]) and gather_ok),
+                             "instances": int(total)}
+            out["roofline"] = None
+            out["cpu_baseline"] = None
+        else:
+            eff_name = f"mpcqp::wv::scale_kernel<{N}> + mpcqp::wv::wave_kernel<{N}>"
+            flops = algorithmic_flops(N, local_res["iters"], local_res["rho_updates"])  # rank 0's launch
+            achieved = flops / (kern_ms * 1e-3) / 1e12
+            key = f"N{N}_B{B}_{args.gait}{'_mu' if args.mixed_mu else ''}"
+            out["roofline"] = {
+                "bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP64_PEAK_TFLOPS, "traffic": load_traffic(key, eff_name),
+                "kernel": eff_name, "kernel_ms": kern_ms, "algorithmic_flop_per_launch": flops,
+                "note": "binary64; the ADMM iterations run on the VALU (v_fmac_f64 DPP mat-vecs) and bound "
+                        "the solve, the Riccati factorization runs on v_mfma_f64_16x16x4f64; peak = FP64 "
+                        "vector spec (equal to the FP64 MFMA peak on gfx950)"}
+            pyoracle = None
+            if not args.no_cpu:
+                pyoracle = oracle_module()
+                op = pyoracle.default_params(N, q=list(params.q_weights), r=list(params.r_weights))
+                S = min(PARITY_SAMPLE, total)
+                idx = np.unique(np.linspace(0, total - 1, S).astype(np.int64))  # every shard represented
+                ref = pyoracle.solve_batch(op, recs_global[idx], nthreads=min(16, os.cpu_count() or 1))
+                out["parity"] = parity_of(res_all[idx], ref)
+                out["parity"]["sample"] = f"{len(idx)} robots evenly spaced over the global batch"
+                out["parity"]["gathered_u0_equals_rank_results"] = gather_ok
+                if world == 1:
+                    out["cpu_baseline"] = cpu_baseline(pyoracle, op, recs_np, args)
+            else:
+                out["parity"] = None
+            out["cpu_baseline"] = out.get("cpu_baseline")
+            out["stats"] = {"mean_iters": float(res_all["iters"].mean()), "max_iters": int(res_all["iters"].max()),
+                            "mean_rho_updates": float(res_all["rho_updates"].mean()),
+                            "solved_frac": float(np.mean(res_all["status"] == 1))}
+            if world == 1 and not args.no_extras:
+                out["extras"] = extras(args, solver, params, recs_np, states, local_res, pyoracle, dev)
+    if solver is not None:
+        solver.close()
     if world > 1:
         dist.destroy_process_group()
+    return out
+
+
+def cpu_baseline(pyoracle, op, recs_np, args):
+    S = min(args.cpu_sample, recs_np.shape[0])
+    nthr = args.cpu_threads or min(16, os.cpu_count() or 1)
+    pyoracle.solve_batch(op, recs_np[:min(S, 64)], nthreads=nthr)  # warm
+    tc = time.perf_counter()
+    pyoracle.solve_batch(op, recs_np[:S], nthreads=nthr)
+    tcpu = time.perf_counter() - tc
+    t1 = time.perf_counter()
+    n1 = min(S, 128)
+    pyoracle.solve_batch(op, recs_np[:n1], nthreads=1)
+    t1 = (time.perf_counter() - t1) / n1
+    return {"value": S / tcpu, "unit": "QP/s", "cores": nthr, "kind": "port",
+            "sample": f"first {S} instances of this workload (same seed) on oracle/mpc_oracle.c "
+                      f"(binary64 ConvexMpc + OSQP-0.6 restatement), {nthr} host threads; "
+                      f"single-thread {t1 * 1e6:.0f} us/QP",
+            "single_thread_us_per_qp": t1 * 1e6}
+
+
+def _timed(fn, steps, stream):
+    """mean ms per call of fn() between HIP events on `stream` (one warm call first)."""
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    for _ in range(steps):
+        fn()
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / steps
+
+
+def extras(args, solver, params, recs_np, states, base_res, pyoracle, dev):
+    """N = 1 extra keys (SURVEY §8(d) end-to-end figures, configs C4 / C5, warm ticks)."""
+    import torch
+    import mpcqp
+    from mpcqp.records import synthetic_go1_ticks
+
+    N, B = args.horizon, recs_np.shape[0]
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    RD = mpcqp._lib.RESULT_DOUBLES
+    steps = max(3, args.steps // 2)
+    nthr = min(16, os.cpu_count() or 1)
+    ex = {}
+
+    def res_of(t):
+        return np.frombuffer(t.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE).copy()
+
+    # -- e2e: host records in, host results out, through the C ABI's host wrapper -------------
+    h_rec = torch.from_numpy(recs_np).pin_memory()
+    h_res = torch.zeros((B, RD), dtype=torch.float64).pin_memory()
+    solver.solve_host_ptr(h_rec.data_ptr(), B, h_res.data_ptr())
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        solver.solve_host_ptr(h_rec.data_ptr(), B, h_res.data_ptr())
+    ms_pin = (time.perf_counter() - t0) / steps * 1e3
+    got_pin = np.frombuffer(h_res.numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
+    res_pg = solver.solve_host(recs_np)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res_pg = solver.solve_host(recs_np)
+    ms_pg = (time.perf_counter() - t0) / steps * 1e3
+    ex["e2e"] = {"value": B / (ms_pin * 1e-3), "unit": "QP/s", "ms_per_call": ms_pin,
+                 "what": "mpcqp_solve_batch_host: pinned host records -> H2D -> solve -> D2H of the "
+                         "results, synchronous (wall clock per call)",
+                 "pageable_value": B / (ms_pg * 1e-3), "pageable_ms_per_call": ms_pg,
+                 "bytes_h2d": int(recs_np.nbytes), "bytes_d2h": int(B * mpcqp.RESULT_DTYPE.itemsize),
+                 "parity": {"bitwise_equal_device_path": bool(
+                     np.array_equal(as_rows(got_pin), as_rows(base_res)) and
+                     np.array_equal(as_rows(res_pg), as_rows(base_res)))}}
+
+    # -- assemble_e2e: raw *CtrlStates rows resident in HBM -> assembly kernel -> solve ---------
+    d_st = torch.from_numpy(mpcqp.pack_states(states)[:B]).to(dev)
+    d_rec2 = torch.zeros((B, mpcqp.rec_size(N)), dtype=torch.float64, device=dev)
+    d_res2 = torch.zeros((B, RD), dtype=torch.float64, device=dev)
+
+    def asm_solve():
+        mpcqp.assemble_records_device(N, d_st.data_ptr(), B, d_rec2.data_ptr(), sp)
+        solver.solve_device(d_rec2.data_ptr(), B, d_res2.data_ptr(), 0, sp)
+    ms = _timed(asm_solve, steps, stream)
+    ex["assemble_e2e"] = {"value": B / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms,
+                          "what": "mpcqp_assemble_records_device + mpcqp_solve_batch_device (HIP events)",
+                          "parity": {"records_bitwise_equal_host_assembly": bool(
+                              np.array_equal(d_rec2.cpu().numpy(), recs_np)),
+                              "u0_bitwise_equal_device_path": bool(
+                              np.array_equal(res_of(d_res2)["u0"], base_res["u0"]))}}
+
+    # -- C5: mixed gait, per-robot contacts ~ Bernoulli(0.5)^4 and mu ~ U(0.3, 0.9), 8192 robots -
+    B5 = 8192
+    st5, rec5 = workload(10, B5, "mixed", True)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10), device=dev.index) as s5:
+        s5.reserve(B5)
+        d5 = torch.from_numpy(rec5).to(dev)
+        r5 = torch.zeros((B5, RD), dtype=torch.float64, device=dev)
+        ms = _timed(lambda: s5.solve_device(d5.data_ptr(), B5, r5.data_ptr(), 0, sp), steps, stream)
+        g5 = res_of(r5)
+    ent = {"value": B5 / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms, "batch": B5, "horizon": 10,
+           "workload": "C5: mixed gait, contacts ~ Bernoulli(0.5)^4, mu ~ U(0.3,0.9)",
+           "mean_iters": float(g5["iters"].mean())}
+    if pyoracle is not None:
+        idx = np.unique(np.linspace(0, B5 - 1, 512).astype(np.int64))
+        ref = pyoracle.solve_batch(pyoracle.default_params(10), rec5[idx], nthreads=nthr)
+        ent["parity"] = parity_of(g5[idx], ref)
+    ex["c5"] = ent
+
+    # -- C4: horizon 20, 4096 trot robots --------------------------------------------------------
+    B4 = 4096
+    st4, rec4 = workload(20, B4, "trot", False)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(20), device=dev.index) as s4:
+        s4.reserve(B4)
+        d4 = torch.from_numpy(rec4).to(dev)
+        r4 = torch.zeros((B4, RD), dtype=torch.float64, device=dev)
+        ms = _timed(lambda: s4.solve_device(d4.data_ptr(), B4, r4.data_ptr(), 0, sp), max(3, steps // 2), stream)
+        g4 = res_of(r4)
+    fl = algorithmic_flops(20, g4["iters"], g4["rho_updates"])
+    ent = {"value": B4 / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms, "batch": B4, "horizon": 20,
+           "workload": "C4: horizon 20 (n=240, m=400), trot", "mean_iters": float(g4["iters"].mean()),
+           "roofline_frac": fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS}
+    if pyoracle is not None:
+        idx = np.unique(np.linspace(0, B4 - 1, 256).astype(np.int64))
+        ref = pyoracle.solve_batch(pyoracle.default_params(20), rec4[idx], nthreads=nthr)
+        ent["parity"] = parity_of(g4[idx], ref)
+    ex["c4"] = ent
+
+    # -- warm_tick: the production tick sequence (persistent warm-started solver per robot) ------
+    T = 10
+    ticks = synthetic_go1_ticks(B, T, seed=31, gait="trot", swing_ticks=5)
+    recs_t = np.stack([mpcqp.assemble_compute_grf(s, N) for s in ticks])
+    d_t = torch.from_numpy(recs_t).to(dev)
+    d_w = torch.zeros((B, solver.warm_state_size), dtype=torch.float64, device=dev)
+    d_rw = torch.zeros((T, B, RD), dtype=torch.float64, device=dev)
+    d_rc = torch.zeros((T, B, RD), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(stream)
+    for t in range(T):
+        solver.solve_warm_device(d_t[t].data_ptr(), B, d_w.data_ptr(), d_rw[t].data_ptr(), 0, sp)
+    ev[1].record(stream)
+    ev[2].record(stream)
+    for t in range(T):
+        solver.solve_device(d_t[t].data_ptr(), B, d_rc[t].data_ptr(), 0, sp)
+    ev[3].record(stream)
+    torch.cuda.synchronize()
+    ms_w = ev[0].elapsed_time(ev[1]) / T
+    ms_c = ev[2].elapsed_time(ev[3]) / T
+    gw = np.frombuffer(d_rw.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE).reshape(T, B)
+    gc = np.frombuffer(d_rc.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE).reshape(T, B)
+    ent = {"value": B / (ms_w * 1e-3), "unit": "QP/s", "ms_per_tick": ms_w, "ticks": T, "batch": B,
+           "cold_ms_per_tick": ms_c, "mean_iters_warm_ticks_2_on": float(gw[1:]["iters"].mean()),
+           "mean_iters_cold": float(gc[1:]["iters"].mean()),
+           "what": "mpcqp_solve_batch_warm_device over consecutive ticks (OsqpEigen warm start: update_P "
+                   "or re-init per robot), synthetic closed-loop trot trajectories"}
+    if pyoracle is not None:
+        nb = 64
+        ref = pyoracle.solve_sequence(pyoracle.default_params(N), np.ascontiguousarray(recs_t[:, :nb]),
+                                      nthreads=nthr)
+        errs = [parity_of(gw[t, :nb], ref[t]) for t in range(T)]
+        ent["parity"] = {"robots": nb, "ticks": T,
+                         "max_rel_err_u0": max(e["max_rel_err_u0"] for e in errs),
+                         "status_equal": all(e["status_equal"] for e in errs),
+                         "iters_equal_frac": float(np.mean([e["iters_equal_frac"] for e in errs]))}
+    ex["warm_tick"] = ent
+    return ex
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    from mpcqp.distributed import env_rank, launch_ranks
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launcher: this process never touches the GPU; the ranks each open their own device
+        return launch_ranks(os.path.abspath(__file__), sys.argv[1:] if argv is None else argv, args.gpus)
+    out = run_rank(args)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

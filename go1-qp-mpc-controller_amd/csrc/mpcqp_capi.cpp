@@ -22,8 +22,12 @@ struct mpcqp_handle {
   double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
   size_t work_per = 0;       // doubles per instance the workspace was sized for
-  int path = 0;              // 0 auto, 1 dense K^-1, 2 Riccati workgroup, 3 Riccati wave, 4 wave per round, 5 register K^-1 (mpcqp_debug_set_solver)
-  // host wrapper staging
+  int path = 0;              // 0 auto (= 3), 3 Riccati wave; debug library only: 1 dense K^-1, 2 Riccati workgroup
+  // host wrapper: device buffers, a private stream and two pinned staging chunks
+  hipStream_t hstream = nullptr;
+  char* pin[2] = {nullptr, nullptr};
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  bool pin_busy[2] = {false, false};
   double* d_recs = nullptr;
   mpcqp_result* d_res = nullptr;
   double* d_sol = nullptr;
@@ -72,26 +76,24 @@ bool params_valid(const mpcqp_params* p) {
   return true;
 }
 
-// 1 dense K^-1, 2 Riccati (one workgroup per robot), 3 Riccati (one wave per robot), 4 Riccati (one
-// wave per horizon round)
-int effective_path(const mpcqp_handle* h) {
-  if (h->path != 0) return h->path;
-  return h->p.horizon <= mpcqp::WAVE_MAX_HORIZON ? 3 : 2;
-}
+// 3 = scale_kernel + wave_kernel (the product path); 1, 2 = cross-check solvers of the debug build
+int effective_path(const mpcqp_handle* h) { return h->path != 0 ? h->path : 3; }
 size_t work_per_instance(const mpcqp_handle* h) {
   switch (effective_path(h)) {
+#ifdef MPCQP_DEBUG_PATHS
     case 1: return mpcqp::workspace_doubles(h->p.horizon);
     case 2: return mpcqp::riccati_workspace_doubles(h->p.horizon);
+#endif
     default: return mpcqp::scale_image_doubles(h->p.horizon);  // scale_kernel -> wave_kernel hand-off
   }
 }
 hipError_t occupancy_for(const mpcqp_handle* h, int* per_cu) {
   switch (effective_path(h)) {
+#ifdef MPCQP_DEBUG_PATHS
     case 1: return mpcqp::occupancy_any(h->p.horizon, per_cu);
     case 2: return mpcqp::occupancy_riccati_any(h->p.horizon, per_cu);
-    case 3: return mpcqp::occupancy_wave_any(h->p.horizon, per_cu);
-    case 5: return mpcqp::occupancy_dx_any(h->p.horizon, per_cu);
-    default: return mpcqp::occupancy_mw_any(h->p.horizon, per_cu);
+#endif
+    default: return mpcqp::occupancy_wave_any(h->p.horizon, per_cu);
   }
 }
 // (Re)size the per-instance workspace for `batch` instances of the current path.
@@ -110,6 +112,72 @@ hipError_t ensure_workspace(mpcqp_handle* h, int32_t batch, void* stream) {
     h->work_cap = cap;
     h->work_per = per;
   }
+  return e;
+}
+
+constexpr size_t PIN_CHUNK = (size_t)2 << 20;  // bytes per pinned staging chunk
+
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+// The host wrappers' private non-blocking stream and pinned staging, created on first use.
+hipError_t ensure_host_io(mpcqp_handle* h) {
+  hipError_t e = hipSuccess;
+  if (!h->hstream) e = hipStreamCreateWithFlags(&h->hstream, hipStreamNonBlocking);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+    if (!h->pin[i]) e = hipHostMalloc((void**)&h->pin[i], PIN_CHUNK, hipHostMallocDefault);
+    if (e == hipSuccess && !h->pin_ev[i]) e = hipEventCreateWithFlags(&h->pin_ev[i], hipEventDisableTiming);
+  }
+  return e;
+}
+
+// Host -> device on the wrapper stream.  A pinned source goes by one DMA; a pageable one through
+// the two staging chunks, the host copy of chunk c + 1 overlapping the DMA of chunk c.
+hipError_t copy_h2d(mpcqp_handle* h, void* dst, const void* src, size_t bytes) {
+  if (host_pinned(src)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->hstream);
+  hipError_t e = hipSuccess;
+  for (size_t off = 0, c = 0; off < bytes && e == hipSuccess; off += PIN_CHUNK, ++c) {
+    const int s = (int)(c & 1);
+    const size_t len = bytes - off < PIN_CHUNK ? bytes - off : PIN_CHUNK;
+    if (h->pin_busy[s]) e = hipEventSynchronize(h->pin_ev[s]);
+    if (e != hipSuccess) break;
+    memcpy(h->pin[s], (const char*)src + off, len);
+    e = hipMemcpyAsync((char*)dst + off, h->pin[s], len, hipMemcpyHostToDevice, h->hstream);
+    if (e == hipSuccess) e = hipEventRecord(h->pin_ev[s], h->hstream);
+    h->pin_busy[s] = e == hipSuccess;
+  }
+  return e;
+}
+
+// Device -> host on the wrapper stream, synchronous on return (same staging scheme as copy_h2d).
+hipError_t copy_d2h(mpcqp_handle* h, void* dst, const void* src, size_t bytes) {
+  hipError_t e;
+  if (host_pinned(dst)) {
+    e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->hstream);
+    return e == hipSuccess ? hipStreamSynchronize(h->hstream) : e;
+  }
+  // chunk c is copied into staging slot c & 1 while chunk c - 1 is copied out of the other slot
+  e = hipSuccess;
+  const size_t nch = (bytes + PIN_CHUNK - 1) / PIN_CHUNK;
+  for (size_t c = 0; c <= nch && e == hipSuccess; ++c) {
+    if (c < nch) {
+      const size_t off = c * PIN_CHUNK, len = bytes - off < PIN_CHUNK ? bytes - off : PIN_CHUNK;
+      e = hipMemcpyAsync(h->pin[c & 1], (const char*)src + off, len, hipMemcpyDeviceToHost, h->hstream);
+      if (e == hipSuccess) e = hipEventRecord(h->pin_ev[c & 1], h->hstream);
+    }
+    if (e == hipSuccess && c > 0) {
+      const size_t off = (c - 1) * PIN_CHUNK, len = bytes - off < PIN_CHUNK ? bytes - off : PIN_CHUNK;
+      e = hipEventSynchronize(h->pin_ev[(c - 1) & 1]);
+      if (e == hipSuccess) memcpy((char*)dst + off, h->pin[(c - 1) & 1], len);
+    }
+  }
+  h->pin_busy[0] = h->pin_busy[1] = false;
   return e;
 }
 
@@ -182,6 +250,12 @@ int32_t mpcqp_destroy(mpcqp_handle* h) {
   (void)hipFree(h->d_sol);
   (void)hipFree(h->d_bal_recs);
   (void)hipFree(h->d_bal_res);
+  if (h->hstream) (void)hipStreamSynchronize(h->hstream);
+  for (int i = 0; i < 2; ++i) {
+    if (h->pin_ev[i]) (void)hipEventDestroy(h->pin_ev[i]);
+    (void)hipHostFree(h->pin[i]);
+  }
+  if (h->hstream) (void)hipStreamDestroy(h->hstream);
   delete h;
   return MPCQP_OK;
 }
@@ -211,11 +285,11 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   a.stream = stream;
   a.p = h->p;
   switch (effective_path(h)) {
+#ifdef MPCQP_DEBUG_PATHS
     case 1: e = mpcqp::launch_solve_any(a); break;
     case 2: e = mpcqp::launch_riccati_any(a); break;
-    case 3: e = mpcqp::launch_wave_any(a); break;
-    case 5: e = mpcqp::launch_dx_any(a); break;
-    default: e = mpcqp::launch_mw_any(a); break;
+#endif
+    default: e = mpcqp::launch_wave_any(a); break;
   }
   if (e != hipSuccess) return set_hip_error(h, e, "solve_kernel launch");
   return MPCQP_OK;
@@ -250,9 +324,12 @@ int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t
   DeviceGuard dg(h->device);
   hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
+  e = ensure_host_io(h);
+  if (e != hipSuccess) return set_hip_error(h, e, "host staging");
   const size_t rs = (size_t)MPCQP_REC_SIZE(h->p.horizon);
   const size_t n = (size_t)MPCQP_NUM_DOF * h->p.horizon;
   if ((size_t)batch > h->cap) {
+    (void)hipStreamSynchronize(h->hstream);
     (void)hipFree(h->d_recs);
     (void)hipFree(h->d_res);
     (void)hipFree(h->d_sol);
@@ -263,15 +340,14 @@ int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t
     if (e != hipSuccess) return set_hip_error(h, e, "hipMalloc");
     h->cap = batch;
   }
-  e = hipMemcpy(h->d_recs, h_records, sizeof(double) * rs * batch, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return set_hip_error(h, e, "hipMemcpy H2D");
+  e = copy_h2d(h, h->d_recs, h_records, sizeof(double) * rs * batch);
+  if (e != hipSuccess) return set_hip_error(h, e, "records H2D");
   int32_t rc = solve_device_impl(h, h->d_recs, batch, h->d_res, h_solution ? h->d_sol : nullptr,
-                                 nullptr, 0, nullptr);
+                                 nullptr, 0, h->hstream);
   if (rc != MPCQP_OK) return rc;
-  e = hipMemcpy(h_results, h->d_res, sizeof(mpcqp_result) * batch, hipMemcpyDeviceToHost);
-  if (e == hipSuccess && h_solution)
-    e = hipMemcpy(h_solution, h->d_sol, sizeof(double) * n * batch, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return set_hip_error(h, e, "hipMemcpy D2H");
+  e = copy_d2h(h, h_results, h->d_res, sizeof(mpcqp_result) * batch);
+  if (e == hipSuccess && h_solution) e = copy_d2h(h, h_solution, h->d_sol, sizeof(double) * n * batch);
+  if (e != hipSuccess) return set_hip_error(h, e, "results D2H");
   return MPCQP_OK;
 }
 
@@ -331,7 +407,10 @@ int32_t mpcqp_balance_solve_host(mpcqp_handle* h, const mpcqp_balance_params* bp
   DeviceGuard dg(h->device);
   hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
+  e = ensure_host_io(h);
+  if (e != hipSuccess) return set_hip_error(h, e, "host staging");
   if ((size_t)batch > h->bal_cap) {
+    (void)hipStreamSynchronize(h->hstream);
     (void)hipFree(h->d_bal_recs);
     (void)hipFree(h->d_bal_res);
     h->d_bal_recs = nullptr; h->d_bal_res = nullptr; h->bal_cap = 0;
@@ -340,12 +419,12 @@ int32_t mpcqp_balance_solve_host(mpcqp_handle* h, const mpcqp_balance_params* bp
     if (e != hipSuccess) return set_hip_error(h, e, "hipMalloc");
     h->bal_cap = batch;
   }
-  e = hipMemcpy(h->d_bal_recs, h_records, sizeof(double) * MPCQP_BAL_SIZE * batch, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return set_hip_error(h, e, "hipMemcpy H2D");
-  int32_t rc = mpcqp_balance_solve_device(h, bp, h->d_bal_recs, batch, h->d_bal_res, nullptr);
+  e = copy_h2d(h, h->d_bal_recs, h_records, sizeof(double) * MPCQP_BAL_SIZE * batch);
+  if (e != hipSuccess) return set_hip_error(h, e, "records H2D");
+  int32_t rc = mpcqp_balance_solve_device(h, bp, h->d_bal_recs, batch, h->d_bal_res, h->hstream);
   if (rc != MPCQP_OK) return rc;
-  e = hipMemcpy(h_results, h->d_bal_res, sizeof(mpcqp_result) * batch, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return set_hip_error(h, e, "hipMemcpy D2H");
+  e = copy_d2h(h, h_results, h->d_bal_res, sizeof(mpcqp_result) * batch);
+  if (e != hipSuccess) return set_hip_error(h, e, "results D2H");
   return MPCQP_OK;
 }
 
@@ -408,13 +487,17 @@ int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {
 }
 int32_t mpcqp_solve_threads(int32_t horizon) {
   if (horizon < 1 || horizon > MPCQP_MAX_HORIZON) return 0;
-  return horizon <= mpcqp::WAVE_MAX_HORIZON ? 64 : mpcqp::riccati_threads(horizon);
+  return 64;  // one wavefront per robot
 }
 
 int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
-  if (!h || path < 0 || path > 5) return MPCQP_ERR_INVALID_ARG;
-  if ((path == 1 || path == 5) && h->p.horizon > mpcqp::DENSE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
-  if (path >= 3 && h->p.horizon > mpcqp::WAVE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
+  if (!h) return MPCQP_ERR_INVALID_ARG;
+#ifdef MPCQP_DEBUG_PATHS
+  if (path < 0 || path > 3) return MPCQP_ERR_INVALID_ARG;
+  if (path == 1 && h->p.horizon > mpcqp::DENSE_MAX_HORIZON) return MPCQP_ERR_INVALID_ARG;
+#else
+  if (path != 0 && path != 3) return MPCQP_ERR_INVALID_ARG;  // cross-check paths: libmpcqp_debug.so
+#endif
   DeviceGuard dg(h->device);
   hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
@@ -433,11 +516,6 @@ int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
 int32_t mpcqp_debug_wave_selftest(double* d_out, void* stream) {
   if (!d_out) return MPCQP_ERR_INVALID_ARG;
   return mpcqp::wave_selftest(d_out, stream) == hipSuccess ? MPCQP_OK : MPCQP_ERR_HIP;
-}
-
-int32_t mpcqp_debug_dx_selftest(double* d_out, void* stream) {
-  if (!d_out) return MPCQP_ERR_INVALID_ARG;
-  return mpcqp::dx_selftest(d_out, stream) == hipSuccess ? MPCQP_OK : MPCQP_ERR_HIP;
 }
 
 }  // extern "C"

@@ -23,32 +23,29 @@ struct LaunchArgs {
   mpcqp_params p;
 };
 
-hipError_t launch_solve_any(const LaunchArgs& a);
+// Formulation only (mpcqp_build.hip): ConvexMpc::calculate_qp_mats, horizons 1..20
 hipError_t launch_build_any(const LaunchArgs& a, double* P, double* q, double* l, double* u);
-hipError_t occupancy_any(int horizon, int* blocks);
-int solve_threads(int horizon);
-size_t workspace_doubles(int horizon);  // per robot
 
-// Riccati-factored path (mpcqp_riccati.hip): horizons 11..20, and any horizon on request
-hipError_t launch_riccati_any(const LaunchArgs& a);
-hipError_t occupancy_riccati_any(int horizon, int* blocks);
-int riccati_threads(int horizon);
-size_t riccati_workspace_doubles(int horizon);  // per robot
-constexpr int DENSE_MAX_HORIZON = 10;
-
-// One-wave-per-robot Riccati path (mpcqp_wave.hip): horizons 1..WAVE_MAX_HORIZON
+// The solve: scale_kernel + one-wave-per-robot Riccati wave_kernel (mpcqp_wave.hip), horizons
+// 1..WAVE_MAX_HORIZON
 hipError_t launch_wave_any(const LaunchArgs& a);
 hipError_t occupancy_wave_any(int horizon, int* blocks);
 hipError_t wave_selftest(double* d_out, void* stream);
 hipError_t launch_scale_any(const LaunchArgs& a);  // scale_kernel alone (the image in a.work)
-// Wave-per-round path (mpcqp_wave_mw.hip): scale_kernel + mw_kernel, horizons 1..WAVE_MAX_HORIZON
-hipError_t launch_mw_any(const LaunchArgs& a);
-hipError_t occupancy_mw_any(int horizon, int* blocks);
 constexpr int WAVE_MAX_HORIZON = 20;
-// Register-resident K^-1 path (mpcqp_dx.hip): scale_kernel + dx_kernel, horizons 1..DENSE_MAX_HORIZON
-hipError_t launch_dx_any(const LaunchArgs& a);
-hipError_t occupancy_dx_any(int horizon, int* blocks);
-hipError_t dx_selftest(double* d_out, void* stream);
+
+#ifdef MPCQP_DEBUG_PATHS
+// Cross-check solvers, built only into libmpcqp_debug.so (mpcqp_debug_set_solver 1, 2):
+// dense K^-1 workgroup (mpcqp_kernels.hip, N <= DENSE_MAX_HORIZON) and workgroup Riccati
+// (mpcqp_riccati.hip).
+hipError_t launch_solve_any(const LaunchArgs& a);
+hipError_t occupancy_any(int horizon, int* blocks);
+size_t workspace_doubles(int horizon);  // per robot
+hipError_t launch_riccati_any(const LaunchArgs& a);
+hipError_t occupancy_riccati_any(int horizon, int* blocks);
+size_t riccati_workspace_doubles(int horizon);  // per robot
+#endif
+constexpr int DENSE_MAX_HORIZON = 10;
 // doubles per robot of the warm-start slot (mpcqp_wave.hip WarmLayout)
 __host__ __device__ constexpr int warm_state_doubles(int N) {
   return 4 + 3 * 12 * N + 5 * 20 * N + ((12 * N + 63) / 64) * 12 * N;

@@ -1,4 +1,4 @@
-// mpcqp_kernels.hip — CDNA4 (gfx950) kernels of the batched convex-MPC QP engine.
+// mpcqp_kernels.hip — dense K^-1 cross-check solver (debug library only, mpcqp_debug_set_solver 1).
 //
 // One workgroup solves one robot.  Its threads form one 16-lane group per FOOT (4 per horizon
 // step; 40 groups = 640 threads = 10 waves at N = 10).  Group f owns, in registers, the 3 rows of
@@ -822,38 +822,11 @@ __global__ __launch_bounds__(Dim<N>::NT) void solve_kernel(
   }
 }
 
-// Formulation-only kernel (P0 parity / ConvexMpc shim): dense H (row-major n x n), g, l, u.
-template <int N>
-__global__ __launch_bounds__(256) void build_qp_kernel(const double* __restrict__ recs, int batch,
-                                                       double* __restrict__ P, double* __restrict__ q,
-                                                       double* __restrict__ l, double* __restrict__ u,
-                                                       mpcqp_params p) {
-  using Dm = Dim<N>;
-  __shared__ Smem<N> sm;
-  const int inst = blockIdx.x;
-  if (inst >= batch) return;
-  const int t = threadIdx.x;
-  for (int e = t; e < Dm::rec; e += 256) sm.rec[e] = recs[(size_t)inst * Dm::rec + e];
-  __syncthreads();
-  condense<N, 256>(sm, p, P + (size_t)inst * Dm::n * Dm::n, Dm::n);
-  if (t < Dm::n) q[(size_t)inst * Dm::n + t] = sm.qt[t];
-  for (int e = t; e < Dm::m; e += 256) {
-    l[(size_t)inst * Dm::m + e] = sm.lo[e];
-    u[(size_t)inst * Dm::m + e] = sm.hi[e];
-  }
-}
-
 // ---- launch table --------------------------------------------------------------------------
 template <int N>
 static hipError_t launch_solve(const LaunchArgs& a) {
   hipLaunchKernelGGL((solve_kernel<N>), dim3(a.grid), dim3(Dim<N>::NT), 0, (hipStream_t)a.stream, a.recs,
                      a.batch, a.results, a.solution, a.work, a.trace, a.trace_cap, a.p);
-  return hipGetLastError();
-}
-template <int N>
-static hipError_t launch_build(const LaunchArgs& a, double* P, double* q, double* l, double* u) {
-  hipLaunchKernelGGL((build_qp_kernel<N>), dim3(a.batch), dim3(256), 0, (hipStream_t)a.stream, a.recs,
-                     a.batch, P, q, l, u, a.p);
   return hipGetLastError();
 }
 template <int N>
@@ -864,24 +837,11 @@ static hipError_t occupancy(int* blocks) {
 #ifndef MPCQP_FOR_EACH_N
 #define MPCQP_FOR_EACH_N(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10)
 #endif
-// The formulation-only kernel serves every horizon the ABI accepts (the Riccati path's range).
-#define MPCQP_BUILD_FOR_EACH_N(X) \
-  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20)
-
 hipError_t launch_solve_any(const LaunchArgs& a) {
   switch (a.p.horizon) {
 #define CASE(K) \
   case K: return launch_solve<K>(a);
     MPCQP_FOR_EACH_N(CASE)
-#undef CASE
-    default: return hipErrorInvalidValue;
-  }
-}
-hipError_t launch_build_any(const LaunchArgs& a, double* P, double* q, double* l, double* u) {
-  switch (a.p.horizon) {
-#define CASE(K) \
-  case K: return launch_build<K>(a, P, q, l, u);
-    MPCQP_BUILD_FOR_EACH_N(CASE)
 #undef CASE
     default: return hipErrorInvalidValue;
   }

@@ -2,7 +2,8 @@
 
 The shared library is built in-tree (go1-qp-mpc-controller_amd/lib/libmpcqp.so) by
 ``make -C go1-qp-mpc-controller_amd`` / ``__graft_entry__.build()``.  There is no fallback:
-if the library is missing or has no HIP device, the call fails loudly.
+if the library is missing or has no HIP device, the call fails loudly.  ``load(debug=True)``
+opens lib/libmpcqp_debug.so instead: the same ABI plus the cross-check solvers (tests only).
 """
 import ctypes
 import os
@@ -12,11 +13,12 @@ import numpy as np
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # MPCQP_LIB overrides the in-tree library (A/B kernel experiments only).
 LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(PKG_ROOT, "lib", "libmpcqp.so")
+DEBUG_LIB_PATH = os.path.join(PKG_ROOT, "lib", "libmpcqp_debug.so")
 
 STATE_DIM, NUM_LEG, NUM_DOF, CONSTRAINT_DIM = 13, 4, 12, 20
 MAX_HORIZON = 20
 DENSE_MAX_HORIZON = 10  # the dense K^-1 path (debug selection) serves horizons up to this
-SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI, SOLVER_WAVE, SOLVER_WAVE_MW, SOLVER_DX = 0, 1, 2, 3, 4, 5
+SOLVER_AUTO, SOLVER_DENSE, SOLVER_RICCATI, SOLVER_WAVE = 0, 1, 2, 3  # 1, 2: debug library only
 OSQP_INFTY = 1e30
 
 # record layout (include/mpcqp.h MPCQP_REC_*)
@@ -99,27 +101,27 @@ EXPORTED = [
     "mpcqp_solve_batch_device", "mpcqp_solve_batch_host", "mpcqp_build_qp_device",
     "mpcqp_status_str", "mpcqp_error_str", "mpcqp_last_error",
     "mpcqp_debug_solve_trace_device", "mpcqp_abi_sizes", "mpcqp_handle_slots", "mpcqp_solve_threads",
-    "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_debug_dx_selftest", "mpcqp_joint_torques_device",
+    "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_joint_torques_device",
     "mpcqp_warm_state_size", "mpcqp_solve_batch_warm_device",
     "mpcqp_balance_default_params", "mpcqp_balance_solve_device", "mpcqp_assemble_records_device",
     "mpcqp_balance_solve_host",
 ]
 
-_lib = None
+_libs = {}
 
 
 class MpcQpError(RuntimeError):
     pass
 
 
-def load():
-    """Load libmpcqp.so (raises if it has not been built)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise MpcQpError(f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` (or __graft_entry__.build())")
-    L = ctypes.CDLL(LIB_PATH)
+def load(debug=False):
+    """Load libmpcqp.so, or libmpcqp_debug.so with debug=True (raises if it has not been built)."""
+    if debug in _libs:
+        return _libs[debug]
+    path = DEBUG_LIB_PATH if debug else LIB_PATH
+    if not os.path.exists(path):
+        raise MpcQpError(f"{path} not built: run `make -C {PKG_ROOT}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(path)
     vp, dp, i32 = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int32
     L.mpcqp_default_params.argtypes = [ctypes.POINTER(Params), i32]
     L.mpcqp_default_params.restype = None
@@ -155,8 +157,6 @@ def load():
     L.mpcqp_debug_set_solver.restype = i32
     L.mpcqp_debug_wave_selftest.argtypes = [vp, vp]
     L.mpcqp_debug_wave_selftest.restype = i32
-    L.mpcqp_debug_dx_selftest.argtypes = [vp, vp]
-    L.mpcqp_debug_dx_selftest.restype = i32
     L.mpcqp_joint_torques_device.argtypes = [vp, vp, i32, vp, vp, vp]
     L.mpcqp_joint_torques_device.restype = i32
     L.mpcqp_warm_state_size.argtypes = [i32]
@@ -176,7 +176,7 @@ def load():
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):
         raise MpcQpError(f"ABI mismatch: C sizes {ps.value}/{rs.value} vs ctypes "
                          f"{ctypes.sizeof(Params)}/{ctypes.sizeof(Result)}")
-    _lib = L
+    _libs[debug] = L
     return L
 
 
@@ -213,9 +213,9 @@ def default_balance_params(**over):
     return bp
 
 
-def check(rc, handle=None, what="mpcqp"):
+def check(rc, handle=None, what="mpcqp", lib=None):
     if rc != ERR_OK:
-        L = load()
+        L = lib or load()
         msg = L.mpcqp_error_str(rc).decode()
         if handle:
             msg += ": " + L.mpcqp_last_error(handle).decode()

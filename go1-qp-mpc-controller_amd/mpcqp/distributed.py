@@ -5,7 +5,16 @@ exchange is one all-gather of the solved first-step forces u0 (12 doubles per ro
 holds the whole batch's GRFs (north_star: "RCCL all-gather of solved ground-reaction forces over
 xGMI").  One process per GPU; torch.distributed with backend "nccl" (= RCCL on ROCm) on the GPUs,
 "gloo" in the CPU tests.
+
+``launch_ranks`` starts those processes from a parent that never touches the GPU: it runs
+``python -m torch.distributed.run`` as a CHILD process (never an exec of the current process) and
+returns its exit code.
 """
+import os
+import socket
+import subprocess
+import sys
+
 import torch
 import torch.distributed as dist
 
@@ -20,19 +29,59 @@ def shard_range(total, world, rank):
 
 
 def allgather_forces(local, total, group=None):
-    """All-gather per-rank [b_r, 12] force rows into [total, 12] on every rank.
+    """All-gather per-rank [b_r, k] rows (u0: k = 12) into [total, k] on every rank.
 
     Shards may differ by one row (balanced split); they are padded to ceil(total/world) for a
-    single all_gather_into_tensor and the padding is stripped.
+    single all_gather_into_tensor and the padding is stripped.  With a balanced split into equal
+    shards no padding copy is made.
     """
     world = dist.get_world_size(group)
     chunk = -(-total // world)
-    pad = torch.zeros((chunk, local.shape[1]), dtype=local.dtype, device=local.device)
-    pad[: local.shape[0]] = local
+    if local.shape[0] == chunk and local.is_contiguous():
+        pad = local
+    else:
+        pad = torch.zeros((chunk, local.shape[1]), dtype=local.dtype, device=local.device)
+        pad[: local.shape[0]] = local
     out = torch.empty((world * chunk, local.shape[1]), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(out, pad, group=group)
+    if chunk * world == total:
+        return out
     rows = []
     for r in range(world):
         b, e = shard_range(total, world, r)
         rows.append(out[r * chunk: r * chunk + (e - b)])
     return torch.cat(rows, 0)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(script, argv, nproc, port):
+    """torch.distributed.run command line: one process per GPU of one node, rendezvous on
+    127.0.0.1 (the container hostname may not resolve)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={int(nproc)}",
+            "--master-addr", "127.0.0.1", "--master-port", str(int(port)), script] + list(argv)
+
+
+def launch_ranks(script, argv, nproc, env=None, port=None):
+    """Run `script argv` on `nproc` ranks as a child process tree; returns the exit code.
+
+    The caller must not have initialised the GPU (no HIP call, no torch.cuda.is_available()):
+    the ranks each open their own device."""
+    e = dict(os.environ if env is None else env)
+    e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK"):
+        e.pop(k, None)
+    cmd = launcher_cmd(script, argv, nproc, port or free_port())
+    return subprocess.call(cmd, env=e)
+
+
+def env_rank():
+    """(world, rank, local_rank) from the torch.distributed.run environment (1, 0, 0 when absent)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))

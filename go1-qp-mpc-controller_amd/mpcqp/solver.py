@@ -14,8 +14,9 @@ from ._lib import RESULT_DTYPE, Params, check, load, rec_size
 
 
 class MpcQpSolver:
-    def __init__(self, params: Params = None, horizon=10, device=0):
-        L = load()
+    def __init__(self, params: Params = None, horizon=10, device=0, debug=False):
+        """debug=True: the handle lives in libmpcqp_debug.so (adds the cross-check solvers)."""
+        L = load(debug)
         self.params = params if params is not None else _lib.default_params(horizon)
         self.horizon = self.params.horizon
         self.n = 12 * self.horizon
@@ -49,23 +50,24 @@ class MpcQpSolver:
         return self._L.mpcqp_handle_slots(self._h)
 
     def set_solver(self, path):
-        """mpcqp_debug_set_solver: 0 auto, 1 dense K^-1 (N <= 10), 2 Riccati workgroup, 3 Riccati wave."""
-        check(self._L.mpcqp_debug_set_solver(self._h, int(path)), self._h, "mpcqp_debug_set_solver")
+        """mpcqp_debug_set_solver: 0 auto, 3 Riccati wave; debug handles also 1 dense K^-1 (N <= 10),
+        2 Riccati workgroup."""
+        check(self._L.mpcqp_debug_set_solver(self._h, int(path)), self._h, "mpcqp_debug_set_solver", self._L)
 
     def reserve(self, batch):
-        check(self._L.mpcqp_reserve(self._h, int(batch)), self._h, "mpcqp_reserve")
+        check(self._L.mpcqp_reserve(self._h, int(batch)), self._h, "mpcqp_reserve", self._L)
 
     # -- device-pointer API ------------------------------------------------------------------------
     def solve_device(self, d_records, batch, d_results, d_solution=0, stream=0):
         """mpcqp_solve_batch_device: records/results/solution are device pointers (ints)."""
         check(self._L.mpcqp_solve_batch_device(self._h, d_records, int(batch), d_results,
                                                d_solution or None, stream or None),
-              self._h, "mpcqp_solve_batch_device")
+              self._h, "mpcqp_solve_batch_device", self._L)
 
     def balance_solve_device(self, bp, d_records, batch, d_results, stream=0):
         """Single-step QP balance controller (mpcqp_balance_solve_device): records [batch][72]."""
         check(self._L.mpcqp_balance_solve_device(self._h, ctypes.byref(bp), d_records, int(batch),
-                                                 d_results, stream or None), self._h, "mpcqp_balance_solve_device")
+                                                 d_results, stream or None), self._h, "mpcqp_balance_solve_device", self._L)
 
     @property
     def warm_state_size(self):
@@ -77,18 +79,18 @@ class MpcQpSolver:
         (A1RobotControl.cpp:522-540); d_state [batch][warm_state_size] doubles, zeroed at first."""
         check(self._L.mpcqp_solve_batch_warm_device(self._h, d_records, int(batch), d_state, d_results,
                                                     d_solution or None, stream or None),
-              self._h, "mpcqp_solve_batch_warm_device")
+              self._h, "mpcqp_solve_batch_warm_device", self._L)
 
     def solve_device_trace(self, d_records, batch, d_results, d_solution, d_trace, trace_cap, stream=0):
         check(self._L.mpcqp_debug_solve_trace_device(self._h, d_records, int(batch), d_results,
                                                      d_solution or None, d_trace, int(trace_cap),
                                                      stream or None),
-              self._h, "mpcqp_debug_solve_trace_device")
+              self._h, "mpcqp_debug_solve_trace_device", self._L)
 
     def build_qp_device(self, d_records, batch, d_P, d_q, d_l, d_u, stream=0):
         check(self._L.mpcqp_build_qp_device(self._h, d_records, int(batch), d_P, d_q, d_l, d_u,
                                             stream or None),
-              self._h, "mpcqp_build_qp_device")
+              self._h, "mpcqp_build_qp_device", self._L)
 
     # -- host convenience --------------------------------------------------------------------------
     def solve_host(self, records, want_solution=False):
@@ -100,5 +102,13 @@ class MpcQpSolver:
         dp = ctypes.POINTER(ctypes.c_double)
         check(self._L.mpcqp_solve_batch_host(
             self._h, recs.ctypes.data_as(dp), B, res.ctypes.data,
-            sol.ctypes.data_as(dp) if sol is not None else None), self._h, "mpcqp_solve_batch_host")
+            sol.ctypes.data_as(dp) if sol is not None else None), self._h, "mpcqp_solve_batch_host", self._L)
         return (res, sol) if want_solution else res
+
+    def solve_host_ptr(self, h_records, batch, h_results, h_solution=0):
+        """mpcqp_solve_batch_host on raw host pointers (ints).  Pinned (hipHostMalloc'd / torch
+        pin_memory) buffers go by one DMA each way; pageable ones through the handle's staging."""
+        dp = ctypes.POINTER(ctypes.c_double)
+        check(self._L.mpcqp_solve_batch_host(self._h, ctypes.cast(h_records, dp), int(batch), h_results,
+                                             ctypes.cast(h_solution, dp) if h_solution else None),
+              self._h, "mpcqp_solve_batch_host", self._L)

@@ -28,17 +28,15 @@ int32_t mpcqp_handle_slots(mpcqp_handle* h);
 /* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */
 int32_t mpcqp_solve_threads(int32_t horizon);
 
-/* Select the linear-system path of a handle: 0 auto (= 3), 1 dense K^-1 (N <= 10), 2 Riccati
- * with one workgroup per robot, 3 Riccati with one wavefront per robot (the default), 4 Riccati
- * with one wave per horizon round, 5 register-resident explicit K^-1 (N <= 10).  All paths run
- * the same OSQP iteration; the selection exists to cross-check them on the same inputs. */
+/* Select the linear-system path of a handle: 0 auto (= 3), 3 Riccati with one wavefront per
+ * robot (the product path).  The debug build libmpcqp_debug.so adds two cross-check solvers:
+ * 1 dense K^-1 with one workgroup per robot (N <= 10), 2 Riccati with one workgroup per robot.
+ * All paths run the same OSQP iteration; the selection exists to cross-check them on the same
+ * inputs.  The product libmpcqp.so returns MPCQP_ERR_INVALID_ARG for 1 and 2. */
 int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path);
 
 /* Cross-lane primitive self-test of the wave path: writes 6 x 64 doubles to d_out (device). */
 int32_t mpcqp_debug_wave_selftest(double* d_out, void* stream);
-
-/* Cross-lane primitive self-test of path 5 (row shifts, broadcast blocks): 6 x 64 doubles. */
-int32_t mpcqp_debug_dx_selftest(double* d_out, void* stream);
 
 #ifdef __cplusplus
 }

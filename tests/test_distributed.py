@@ -60,3 +60,26 @@ def test_shard_range_partitions():
             assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
             sizes = [e - b for b, e in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("world,batch", [(2, 48), (3, 16)])
+def test_bench_launcher_shards_and_gathers(world, batch):
+    """bench.py --gpus N as the driver runs it: the parent starts torch.distributed.run as a child
+    (no GPU touched), N ranks take contiguous shards of ONE seeded global batch, run the production
+    per-step call path (solve -> mpcqp.distributed.allgather_forces, here over gloo with a CPU stub
+    in place of the device solve) and rank 0 checks the world size and the gathered forces."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(world), "--cpu-stub",
+                          "--steps", "2", "--warmup", "1", "--batch", str(batch)],
+                         capture_output=True, text=True, timeout=300, cwd=repo)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == world and rec["config"]["ranks_seen"] == world
+    assert rec["config"]["global_batch"] == world * batch
+    assert rec["parity"]["gather_exact"] and rec["parity"]["instances"] == world * batch
+    assert rec["value"] > 0 and rec["scaling"] == "weak"

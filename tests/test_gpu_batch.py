@@ -50,3 +50,45 @@ def test_repeat_solves_are_bitwise_identical(big):
             r2, s2, _ = solve_gpu(s, recs[:777])
             np.testing.assert_array_equal(r2["u0"], res["u0"][:777])
             np.testing.assert_array_equal(s2, sol[:777])
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_solve_equals_single_solve(world):
+    """C3's sharding on one device: the global 8192-robot batch solved as world contiguous
+    shard_range shards (what each rank of bench.py --gpus world solves) and concatenated in rank
+    order (what allgather_forces returns) is bitwise the single-launch solve (bench.py --gpus 1
+    --batch 8192)."""
+    from mpcqp.distributed import shard_range
+    total = 8192
+    st = mpcqp.synthetic_go1(total, seed=1000, gait="trot")
+    recs = mpcqp.assemble_compute_grf(st, 10)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+        whole, _, _ = solve_gpu(s, recs)
+        parts = [solve_gpu(s, recs[b:e])[0] for b, e in (shard_range(total, world, r) for r in range(world))]
+    cat = np.concatenate(parts)
+    np.testing.assert_array_equal(cat["u0"], whole["u0"])
+    np.testing.assert_array_equal(cat["iters"], whole["iters"])
+    np.testing.assert_array_equal(cat["status"], whole["status"])
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_wrapper_equals_device_path(big, pinned):
+    """mpcqp_solve_batch_host (records 9.6 MB and solutions 3.9 MB: several 2-MiB staging chunks
+    each way when pageable, one DMA each way when pinned) returns bitwise the device path's
+    results, on repeated calls."""
+    recs, res, sol = big
+    B = 4096
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+        for _ in range(2):
+            if pinned:
+                h_rec = torch.from_numpy(np.ascontiguousarray(recs[:B])).pin_memory()
+                h_res = torch.zeros((B, mpcqp._lib.RESULT_DOUBLES), dtype=torch.float64).pin_memory()
+                h_sol = torch.zeros((B, s.n), dtype=torch.float64).pin_memory()
+                s.solve_host_ptr(h_rec.data_ptr(), B, h_res.data_ptr(), h_sol.data_ptr())
+                r2 = np.frombuffer(h_res.numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
+                s2 = h_sol.numpy()
+            else:
+                r2, s2 = s.solve_host(recs[:B], want_solution=True)
+            np.testing.assert_array_equal(r2["u0"], res["u0"][:B])
+            np.testing.assert_array_equal(r2["iters"], res["iters"][:B])
+            np.testing.assert_array_equal(s2, sol[:B])

@@ -1,4 +1,4 @@
-"""Riccati linear-system path (horizons 11..20, and any horizon on request) vs the CPU oracle.
+"""Horizons 11..20 on the product path, and the workgroup Riccati cross-check solver (debug library), vs the CPU oracle.
 
 The Riccati path runs the same OSQP 0.6 iteration as the dense path; only the reduced-KKT solve
 (P~ + sigma I + A~' rho A~) x~ = rhs is computed differently (block-tridiagonal LQR recursion
@@ -103,7 +103,7 @@ def test_forced_riccati_small_horizons(oracle, N):
     """The Riccati path on horizons the dense path serves: cross-check both against the oracle."""
     st = mpcqp.synthetic_go1(64, seed=400 + N, gait="mixed", mixed_mu=True)
     recs = mpcqp.assemble_compute_grf(st, N)
-    with mpcqp.MpcQpSolver(mpcqp.default_params(N)) as s:
+    with mpcqp.MpcQpSolver(mpcqp.default_params(N), debug=True) as s:
         s.set_solver(mpcqp._lib.SOLVER_RICCATI)
         _check_p1_riccati(oracle, s, recs, f"riccati N={N}")
         s.set_solver(mpcqp._lib.SOLVER_DENSE)
@@ -114,9 +114,19 @@ def test_forced_riccati_small_horizons(oracle, N):
 
 
 def test_dense_rejected_above_10():
-    with mpcqp.MpcQpSolver(mpcqp.default_params(20)) as s:
+    with mpcqp.MpcQpSolver(mpcqp.default_params(20), debug=True) as s:
         with pytest.raises(mpcqp.MpcQpError):
             s.set_solver(mpcqp._lib.SOLVER_DENSE)
+
+
+@pytest.mark.parametrize("path", [1, 2, 4, 5])
+def test_product_library_has_only_the_wave_path(path):
+    """libmpcqp.so ships only scale_kernel + wave_kernel; the cross-check solvers live in
+    libmpcqp_debug.so and paths 4 / 5 no longer exist."""
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+        with pytest.raises(mpcqp.MpcQpError):
+            s.set_solver(path)
+        s.set_solver(mpcqp._lib.SOLVER_WAVE)
 
 
 def test_n20_converged_p2(oracle):

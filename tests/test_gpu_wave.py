@@ -89,7 +89,7 @@ def test_wave_matches_dense(n10_wave):
     st = mpcqp.synthetic_go1(128, seed=77, gait="mixed", mixed_mu=True)
     recs = mpcqp.assemble_compute_grf(st, 10)
     wave, _, _ = solve_gpu(n10_wave, recs)
-    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10), debug=True) as s:
         s.set_solver(mpcqp._lib.SOLVER_DENSE)
         dense, _, _ = solve_gpu(s, recs)
     assert np.all(rel_err_u0(wave["u0"], dense["u0"]) <= TOL_P1)

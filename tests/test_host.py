@@ -136,3 +136,20 @@ def test_synthetic_generator_is_seeded_and_in_range():
     np.testing.assert_allclose(np.einsum("bij,bkj->bik", R, R), np.broadcast_to(np.eye(3), R.shape), atol=1e-12)
     t = mpcqp.synthetic_go1(4, seed=0, gait="trot")
     assert t.contacts.tolist() == [[True, False, False, True], [False, True, True, False]] * 2
+
+
+def test_product_library_ships_only_the_default_solve():
+    """libmpcqp.so holds the wave path's kernels and none of the cross-check solvers (those are
+    in libmpcqp_debug.so, which exports the same ABI)."""
+    def kernels(path):
+        out = subprocess.run(["nm", "-C", "--defined-only", path], capture_output=True, text=True).stdout
+        return out
+    prod = kernels(_lib.LIB_PATH)
+    dbg = kernels(_lib.DEBUG_LIB_PATH)
+    assert "mpcqp::wv::wave_kernel<10>" in prod and "mpcqp::wv::scale_kernel<10>" in prod
+    for name in ("mpcqp::solve_kernel<", "mpcqp::ric::ric_solve_kernel<", "mw_kernel", "dx_kernel"):
+        assert name not in prod, name
+    assert "mpcqp::solve_kernel<10>" in dbg and "mpcqp::ric::ric_solve_kernel<10>" in dbg
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.DEBUG_LIB_PATH], capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert _declared_functions() <= exported

@@ -13,11 +13,11 @@ mkdir -p "$OUT"
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/gpu_tests.txt" 2>&1
 timeout -k 10 300 python3 bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
-  -- python3 bench.py --steps 10 --warmup 2 --no-cpu "$@" > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof_trace.err"
+  -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-extras "$@" > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof_trace.err"
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "scale_kernel|wave_kernel" --output-format csv \
-  -d "$OUT/pmc/fetch" -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu "$@" > /dev/null 2> "$OUT/rocprof_fetch.err"
+  -d "$OUT/pmc/fetch" -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-extras "$@" > /dev/null 2> "$OUT/rocprof_fetch.err"
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "scale_kernel|wave_kernel" --output-format csv \
-  -d "$OUT/pmc/write" -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu "$@" > /dev/null 2> "$OUT/rocprof_write.err"
+  -d "$OUT/pmc/write" -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-extras "$@" > /dev/null 2> "$OUT/rocprof_write.err"
 tools/iter_cost.sh "$OUT/iter" > "$OUT/iter_cost.txt" 2>&1
 bash tools/pmc_lds.sh "$OUT/lds" > "$OUT/lds_cost.txt" 2>&1
 echo done

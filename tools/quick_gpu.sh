@@ -12,7 +12,7 @@ tail -3 "$OUT/gpu_tests.txt"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
-  -- python3 bench.py --steps 10 --warmup 2 --no-cpu "$@" > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err" || exit $?
+  -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-extras "$@" > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err" || exit $?
 python3 - "$OUT" << 'PY'
 import csv, json, sys
 o = sys.argv[1]

@@ -18,7 +18,7 @@ from gpu_helpers import rel_err_u0, solve_gpu
 def stats(N, path, gait, B=64, seed=5):
     st = mpcqp.synthetic_go1(B, seed=seed, gait=gait, mixed_mu=(gait == "mixed"))
     recs = mpcqp.assemble_compute_grf(st, N)
-    with mpcqp.MpcQpSolver(mpcqp.default_params(N)) as s:
+    with mpcqp.MpcQpSolver(mpcqp.default_params(N), debug=True) as s:
         s.set_solver(path)
         got, _, _ = solve_gpu(s, recs)
     op = pyoracle.default_params(N)
@@ -33,7 +33,7 @@ def stats(N, path, gait, B=64, seed=5):
 def timing(N, path, B=4096, reps=5):
     st = mpcqp.synthetic_go1(B, seed=9, gait="trot")
     recs = mpcqp.assemble_compute_grf(st, N)
-    with mpcqp.MpcQpSolver(mpcqp.default_params(N)) as s:
+    with mpcqp.MpcQpSolver(mpcqp.default_params(N), debug=True) as s:
         s.set_solver(path)
         s.reserve(B)
         d_rec = torch.from_numpy(recs).cuda()
