@@ -264,7 +264,7 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
                                  mpcqp_result* d_results, double* d_solution, double* d_trace,
                                  int32_t trace_cap, void* stream, double* d_state = nullptr) {
   if (!h || batch < 0 || (batch > 0 && (!d_records || !d_results))) return MPCQP_ERR_INVALID_ARG;
-  if (d_state && effective_path(h) < 3) return MPCQP_ERR_INVALID_ARG;  // warm start: wave paths only
+  if (d_state && effective_path(h) != 3) return MPCQP_ERR_INVALID_ARG;  // warm start: the wave path
   if (batch == 0) return MPCQP_OK;
   DeviceGuard dg(h->device);
   hipError_t e = dg.err;
@@ -317,10 +317,11 @@ int32_t mpcqp_solve_batch_warm_device(mpcqp_handle* h, const double* d_records, 
   return solve_device_impl(h, d_records, batch, d_results, d_solution, nullptr, 0, stream, d_state);
 }
 
-int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t batch,
+static int32_t solve_host_impl(mpcqp_handle* h, const double* h_records, int32_t batch, double* d_state,
                                mpcqp_result* h_results, double* h_solution) {
   if (!h || batch < 0 || (batch > 0 && (!h_records || !h_results))) return MPCQP_ERR_INVALID_ARG;
   if (batch == 0) return MPCQP_OK;
+  if (d_state && effective_path(h) != 3) return MPCQP_ERR_INVALID_ARG;  // warm start: the wave path
   DeviceGuard dg(h->device);
   hipError_t e = dg.err;
   if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
@@ -343,12 +344,23 @@ int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t
   e = copy_h2d(h, h->d_recs, h_records, sizeof(double) * rs * batch);
   if (e != hipSuccess) return set_hip_error(h, e, "records H2D");
   int32_t rc = solve_device_impl(h, h->d_recs, batch, h->d_res, h_solution ? h->d_sol : nullptr,
-                                 nullptr, 0, h->hstream);
+                                 nullptr, 0, h->hstream, d_state);
   if (rc != MPCQP_OK) return rc;
   e = copy_d2h(h, h_results, h->d_res, sizeof(mpcqp_result) * batch);
   if (e == hipSuccess && h_solution) e = copy_d2h(h, h_solution, h->d_sol, sizeof(double) * n * batch);
   if (e != hipSuccess) return set_hip_error(h, e, "results D2H");
   return MPCQP_OK;
+}
+
+int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t batch,
+                               mpcqp_result* h_results, double* h_solution) {
+  return solve_host_impl(h, h_records, batch, nullptr, h_results, h_solution);
+}
+
+int32_t mpcqp_solve_batch_warm_host(mpcqp_handle* h, const double* h_records, int32_t batch, double* d_state,
+                                    mpcqp_result* h_results, double* h_solution) {
+  if (batch > 0 && !d_state) return MPCQP_ERR_INVALID_ARG;
+  return solve_host_impl(h, h_records, batch, d_state, h_results, h_solution);
 }
 
 int32_t mpcqp_build_qp_device(mpcqp_handle* h, const double* d_records, int32_t batch, double* d_P,

@@ -104,7 +104,7 @@ EXPORTED = [
     "mpcqp_debug_set_solver", "mpcqp_debug_wave_selftest", "mpcqp_joint_torques_device",
     "mpcqp_warm_state_size", "mpcqp_solve_batch_warm_device",
     "mpcqp_balance_default_params", "mpcqp_balance_solve_device", "mpcqp_assemble_records_device",
-    "mpcqp_balance_solve_host",
+    "mpcqp_balance_solve_host", "mpcqp_solve_batch_warm_host",
 ]
 
 _libs = {}
@@ -163,6 +163,8 @@ def load(debug=False):
     L.mpcqp_warm_state_size.restype = i32
     L.mpcqp_solve_batch_warm_device.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     L.mpcqp_solve_batch_warm_device.restype = i32
+    L.mpcqp_solve_batch_warm_host.argtypes = [vp, dp, i32, vp, vp, dp]
+    L.mpcqp_solve_batch_warm_host.restype = i32
     L.mpcqp_balance_default_params.argtypes = [ctypes.POINTER(BalanceParams)]
     L.mpcqp_balance_default_params.restype = None
     L.mpcqp_balance_solve_device.argtypes = [vp, ctypes.POINTER(BalanceParams), vp, i32, vp, vp]

@@ -156,9 +156,20 @@ int32_t mpcqp_warm_state_size(int32_t horizon);
 int32_t mpcqp_solve_batch_warm_device(mpcqp_handle* h, const double* d_records, int32_t batch, double* d_state,
                                       mpcqp_result* d_results, double* d_solution, void* stream);
 
-/* Host-pointer convenience wrapper (copies in, solves, copies out, synchronizes). */
+/* Host-pointer convenience wrapper (copies in, solves, copies out, synchronizes) on a stream of the
+ * handle's own.  Pinned host buffers (hipHostMalloc / registered) move by one DMA each way;
+ * pageable ones through two pinned 2-MiB staging chunks of the handle, host copies overlapping the
+ * DMA.  Not for concurrent use of one handle from several threads. */
 int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t batch,
                                mpcqp_result* h_results, double* h_solution);
+
+/* Host-pointer variant of the warm-started solve: records and results on the host (as in
+ * mpcqp_solve_batch_host), the solver slots d_state in DEVICE memory (as in
+ * mpcqp_solve_batch_warm_device).  This is the per-tick call of a persistent controller-owned
+ * solver (A1RobotControl.h:67 member OsqpEigen::Solver, warm start on: A1RobotControl.cpp:522-540);
+ * synchronous. */
+int32_t mpcqp_solve_batch_warm_host(mpcqp_handle* h, const double* h_records, int32_t batch, double* d_state,
+                                    mpcqp_result* h_results, double* h_solution);
 
 /* Formulation only (ConvexMpc::calculate_qp_mats): dense Hessian (full symmetric, row-major
  * [12N][12N]), gradient [12N], bounds l/u [20N] per instance.  DEVICE pointers. */

@@ -2,20 +2,30 @@
 // implemented over the C ABI in mpcqp.h (link with libmpcqp.so).
 //
 //   mpcqp_cpp::ConvexMpc<N>          ≙ class ConvexMpc (src/a1_cpp/src/ConvexMpc.h:22-94)
-//   mpcqp_cpp::A1RobotControl        ≙ A1RobotControl::compute_grf MPC branch
-//                                       (src/a1_cpp/src/A1RobotControl.cpp:446-562)
+//   mpcqp_cpp::A1RobotControl        ≙ A1RobotControl::compute_grf (src/a1_cpp/src/A1RobotControl.h:44,
+//                                       MPC branch A1RobotControl.cpp:446-562, QP branch :377-444)
 //   mpcqp_cpp::Go1RobotControl       ≙ the declared-but-undefined Go1 hook
 //                                       (src/go1_rl_ctrl_cpp/src/Go1RLController.hpp:38-40)
 //
-// Eigen-agnostic: state types are templates; anything with operator[] for 3-vectors,
+// Eigen-agnostic: state types are templates; anything with operator[] for vectors,
 // operator()(r,c) for matrices and a bool contacts[4] works (Eigen::Vector3d / Matrix3d /
-// Matrix<double,3,4> included), so A1CtrlStates / Go1CtrlStates plug in unchanged.
+// Matrix<double,3,4> included), so A1CtrlStates / Go1CtrlStates plug in unchanged.  The matrices
+// the shim owns are mpcqp_cpp::Mat<R, C>, which speaks the Eigen spellings the reference's caller
+// uses (m(r, c), m.block<R, C>(i, j) = other) and converts implicitly to any matrix type with
+// operator()(r, c), so `state.foot_forces_grf = ctrl.compute_grf(state, dt);` compiles with an
+// Eigen::Matrix<double, 3, 4> on the left.
 #pragma once
+
+#include <hip/hip_runtime_api.h>
 
 #include <cmath>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "mpcqp.h"
@@ -29,10 +39,188 @@ inline void throw_on(int32_t rc, mpcqp_handle* h, const char* what) {
     throw std::runtime_error(msg);
   }
 }
+inline void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Makes `device` current for a scope and restores the caller's current device (device
+// buffers of a handle must be allocated on the handle's device, whatever the caller's selection).
+class DeviceScope {
+ public:
+  explicit DeviceScope(int device) {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+    hip_ok(hipSetDevice(device), "hipSetDevice");
+  }
+  ~DeviceScope() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+
+ private:
+  int prev_ = -1;
+};
 
 // ---------------------------------------------------------------------------------------------
-// ConvexMpc: same method names and call order as the reference; calculate_qp_mats() runs the
-// formulation on the GPU (mpcqp_build_qp_device) and fills the public members.
+// Mat<R, C>: fixed-size row-major binary64 matrix with the Eigen member spellings of the caller.
+// ---------------------------------------------------------------------------------------------
+template <class M, class = void>
+struct is_matrix_like : std::false_type {};
+template <class M>
+struct is_matrix_like<M, std::void_t<decltype(std::declval<M&>()(0, 0) = 0.0)>> : std::true_type {};
+
+template <int R, int C>
+struct Mat {
+  double a[R * C] = {};
+  static constexpr int rows() { return R; }
+  static constexpr int cols() { return C; }
+  double& operator()(int r, int c) { return a[r * C + c]; }
+  const double& operator()(int r, int c) const { return a[r * C + c]; }
+  double* data() { return a; }
+  const double* data() const { return a; }
+  void setZero() { std::memset(a, 0, sizeof(a)); }
+  static Mat Zero() { return Mat(); }
+
+  template <int BR, int BC>
+  struct Block {  // Eigen's m.block<BR, BC>(r0, c0): read, write, assign from any matrix-like
+    Mat* m;
+    int r0, c0;
+    double& operator()(int r, int c) { return (*m)(r0 + r, c0 + c); }
+    template <class O>
+    Block& operator=(const O& o) {
+      for (int r = 0; r < BR; ++r)
+        for (int c = 0; c < BC; ++c) (*m)(r0 + r, c0 + c) = o(r, c);
+      return *this;
+    }
+    operator Mat<BR, BC>() const {
+      Mat<BR, BC> o;
+      for (int r = 0; r < BR; ++r)
+        for (int c = 0; c < BC; ++c) o(r, c) = (*m)(r0 + r, c0 + c);
+      return o;
+    }
+  };
+  template <int BR, int BC>
+  Block<BR, BC> block(int r0, int c0) {
+    static_assert(BR <= R && BC <= C, "block larger than the matrix");
+    if (r0 < 0 || c0 < 0 || r0 + BR > R || c0 + BC > C) throw std::out_of_range("Mat::block");
+    return Block<BR, BC>{this, r0, c0};
+  }
+  template <int BR, int BC>
+  Mat<BR, BC> block(int r0, int c0) const {
+    return const_cast<Mat*>(this)->template block<BR, BC>(r0, c0);
+  }
+  // assignment from / conversion to any other matrix-like type (e.g. Eigen::Matrix<double, R, C>)
+  template <class O, class = std::enable_if_t<is_matrix_like<O>::value && !std::is_same<O, Mat>::value>>
+  Mat& operator=(const O& o) {
+    for (int r = 0; r < R; ++r)
+      for (int c = 0; c < C; ++c) (*this)(r, c) = o(r, c);
+    return *this;
+  }
+  template <class O, class = std::enable_if_t<is_matrix_like<O>::value && !std::is_same<O, Mat>::value &&
+                                              std::is_default_constructible<O>::value>>
+  operator O() const {
+    O o;
+    for (int r = 0; r < R; ++r)
+      for (int c = 0; c < C; ++c) o(r, c) = (*this)(r, c);
+    return o;
+  }
+};
+using Matrix34 = Mat<3, MPCQP_NUM_LEG>;
+
+namespace detail {
+
+// calculate_B_mat_c + state_space_discretization on the host (ConvexMpc.cpp:132-156, Utils.cpp:
+// 35-41): B_d = B_c dt with B_c rows 6-8 = I_w^-1 [r_l]x, rows 9-11 = I / m (I_w = R I_b R',
+// Eigen's cofactor 3x3 inverse).  The device recomputes the same matrices from the same inputs.
+inline void iw_and_inverse(const double R[9], const double Ib[9], double Iw[9], double Iwinv[9]) {
+  double t[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < 3; ++k) s += R[3 * i + k] * Ib[3 * k + j];
+      t[3 * i + j] = s;
+    }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < 3; ++k) s += t[3 * i + k] * R[3 * j + k];
+      Iw[3 * i + j] = s;
+    }
+  auto cof = [&](int i, int j) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return Iw[3 * i1 + j1] * Iw[3 * i2 + j2] - Iw[3 * i1 + j2] * Iw[3 * i2 + j1];
+  };
+  const double invdet = 1.0 / ((cof(0, 0) * Iw[0] + cof(1, 0) * Iw[3]) + cof(2, 0) * Iw[6]);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Iwinv[3 * j + i] = cof(i, j) * invdet;
+}
+inline void b_mat_c(double mass, const double Iwinv[9], const double feet[12], Mat<13, 12>& B) {
+  B.setZero();
+  for (int l = 0; l < MPCQP_NUM_LEG; ++l) {
+    const double* r = feet + 3 * l;
+    const double sk[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double s = 0.0;
+        for (int k = 0; k < 3; ++k) s += Iwinv[3 * i + k] * sk[3 * k + j];
+        B(6 + i, 3 * l + j) = s;
+      }
+    for (int i = 0; i < 3; ++i) B(9 + i, 3 * l + i) = 1.0 / mass;
+  }
+}
+
+// One formulation handle + device staging per (device, weights), shared by every ConvexMpc
+// object: the reference constructs ConvexMpc on every tick (A1RobotControl.cpp:447), which must
+// not mean a handle and five device allocations per tick.  Entries live for the process (they are
+// intentionally never destroyed: no HIP call from static destructors after runtime teardown).
+template <int N>
+struct BuildSlot {
+  std::mutex mu;
+  int device = 0;
+  double q[MPCQP_STATE_DIM], r[MPCQP_NUM_DOF];
+  mpcqp_handle* h = nullptr;
+  double *d_rec = nullptr, *d_P = nullptr, *d_q = nullptr, *d_l = nullptr, *d_u = nullptr;
+};
+template <int N>
+inline BuildSlot<N>* build_slot(int device, const double* q, const double* r) {
+  static std::mutex pool_mu;
+  static std::vector<BuildSlot<N>*> pool;
+  std::lock_guard<std::mutex> lk(pool_mu);
+  for (BuildSlot<N>* s : pool)
+    if (s->device == device && !std::memcmp(s->q, q, sizeof(s->q)) && !std::memcmp(s->r, r, sizeof(s->r))) return s;
+  std::unique_ptr<BuildSlot<N>> s(new BuildSlot<N>());
+  s->device = device;
+  std::memcpy(s->q, q, sizeof(s->q));
+  std::memcpy(s->r, r, sizeof(s->r));
+  mpcqp_params p;
+  mpcqp_default_params(&p, N);
+  std::memcpy(p.q_weights, q, sizeof(s->q));
+  std::memcpy(p.r_weights, r, sizeof(s->r));
+  throw_on(mpcqp_create(&p, device, &s->h), nullptr, "mpcqp_create");
+  try {
+    DeviceScope ds(device);
+    const int n = MPCQP_NUM_DOF * N, m = MPCQP_CONSTRAINT_DIM * N;
+    hip_ok(hipMalloc(&s->d_rec, sizeof(double) * MPCQP_REC_SIZE(N)), "hipMalloc");
+    hip_ok(hipMalloc(&s->d_P, sizeof(double) * n * n), "hipMalloc");
+    hip_ok(hipMalloc(&s->d_q, sizeof(double) * n), "hipMalloc");
+    hip_ok(hipMalloc(&s->d_l, sizeof(double) * m), "hipMalloc");
+    hip_ok(hipMalloc(&s->d_u, sizeof(double) * m), "hipMalloc");
+  } catch (...) {
+    DeviceScope ds(device);
+    for (double* d : {s->d_rec, s->d_P, s->d_q, s->d_l, s->d_u}) (void)hipFree(d);
+    mpcqp_destroy(s->h);
+    throw;
+  }
+  pool.push_back(s.get());
+  return s.release();
+}
+
+}  // namespace detail
+
+// ---------------------------------------------------------------------------------------------
+// ConvexMpc: same methods, call order and public members as the reference (ConvexMpc.h:22-94).
+// calculate_qp_mats() reads B_mat_d_list (what the caller stored, A1RobotControl.cpp:513) and
+// runs the formulation on the GPU (mpcqp_build_qp_device) to fill hessian / gradient / lb / ub.
 // ---------------------------------------------------------------------------------------------
 template <int N = 10>
 class ConvexMpc {
@@ -41,11 +229,12 @@ class ConvexMpc {
   static constexpr int m = MPCQP_CONSTRAINT_DIM * N;
 
   template <class VecQ, class VecR>
-  ConvexMpc(const VecQ& q_weights_, const VecR& r_weights_, int device = 0) : mu(0.3), fz_min(0), fz_max(0) {
-    mpcqp_default_params(&params_, N);
-    for (int i = 0; i < MPCQP_STATE_DIM; ++i) params_.q_weights[i] = q_weights_[i];
-    for (int i = 0; i < MPCQP_NUM_DOF; ++i) params_.r_weights[i] = r_weights_[i];
-    throw_on(mpcqp_create(&params_, device, &h_), nullptr, "mpcqp_create");
+  ConvexMpc(const VecQ& q_weights_, const VecR& r_weights_, int device = 0)
+      : mu(0.3), fz_min(0), fz_max(0), device_(device) {
+    double q[MPCQP_STATE_DIM], r[MPCQP_NUM_DOF];
+    for (int i = 0; i < MPCQP_STATE_DIM; ++i) q[i] = q_weights_[i];
+    for (int i = 0; i < MPCQP_NUM_DOF; ++i) r[i] = r_weights_[i];
+    slot_ = detail::build_slot<N>(device, q, r);
     hessian.assign((size_t)n * n, 0.0);
     gradient.assign(n, 0.0);
     lb.assign(m, 0.0);
@@ -53,16 +242,18 @@ class ConvexMpc {
     linear_constraints.assign((size_t)m * n, 0.0);
     reset();
   }
-  ~ConvexMpc() {
-    free_device();
-    if (h_) mpcqp_destroy(h_);
-  }
   ConvexMpc(const ConvexMpc&) = delete;
   ConvexMpc& operator=(const ConvexMpc&) = delete;
 
   void reset() {  // ConvexMpc.cpp:70-108
     rec_.assign(MPCQP_REC_SIZE(N), 0.0);
     step_ = 0;
+    have_body_ = false;
+    A_mat_c.setZero();
+    B_mat_c.setZero();
+    A_mat_d.setZero();
+    B_mat_d.setZero();
+    B_mat_d_list.setZero();
     std::fill(gradient.begin(), gradient.end(), 0.0);
     std::fill(lb.begin(), lb.end(), 0.0);
     std::fill(ub.begin(), ub.end(), 0.0);
@@ -71,37 +262,58 @@ class ConvexMpc {
   template <class Vec3>
   void calculate_A_mat_c(const Vec3& root_euler) {  // ConvexMpc.cpp:110-130 (yaw only)
     for (int k = 0; k < 3; ++k) rec_[MPCQP_REC_EULER + k] = root_euler[k];
+    const double cy = std::cos(root_euler[2]), sy = std::sin(root_euler[2]);
+    A_mat_c.setZero();
+    A_mat_c(0, 6) = cy;
+    A_mat_c(0, 7) = sy;
+    A_mat_c(1, 6) = -sy;
+    A_mat_c(1, 7) = cy;
+    A_mat_c(2, 8) = 1.0;
+    for (int i = 0; i < 3; ++i) A_mat_c(3 + i, 9 + i) = 1.0;
+    A_mat_c(11, 12) = 1.0;
   }
 
-  // ConvexMpc.cpp:132-143: the body inertia, rotation and feet of the NEXT horizon step.
+  // ConvexMpc.cpp:132-143.  The record holds ONE mass / inertia / rotation for the horizon (what
+  // both reference callers pass); feet may differ per horizon step.
   template <class Mat3a, class Mat3b, class Mat34>
   void calculate_B_mat_c(double robot_mass, const Mat3a& trunk_inertia, const Mat3b& root_rot_mat,
                          const Mat34& foot_pos) {
-    rec_[MPCQP_REC_MASS] = robot_mass;
+    double R[9], Ib[9];
     for (int r = 0; r < 3; ++r)
       for (int c = 0; c < 3; ++c) {
-        rec_[MPCQP_REC_INERTIA + 3 * r + c] = trunk_inertia(r, c);
-        rec_[MPCQP_REC_ROT + 3 * r + c] = root_rot_mat(r, c);
+        Ib[3 * r + c] = trunk_inertia(r, c);
+        R[3 * r + c] = root_rot_mat(r, c);
       }
+    if (have_body_ && (robot_mass != rec_[MPCQP_REC_MASS] || std::memcmp(Ib, &rec_[MPCQP_REC_INERTIA], sizeof(Ib)) ||
+                       std::memcmp(R, &rec_[MPCQP_REC_ROT], sizeof(R))))
+      throw std::invalid_argument("ConvexMpc: mass, inertia and rotation must be the same for every horizon step");
+    have_body_ = true;
+    rec_[MPCQP_REC_MASS] = robot_mass;
+    std::memcpy(&rec_[MPCQP_REC_INERTIA], Ib, sizeof(Ib));
+    std::memcpy(&rec_[MPCQP_REC_ROT], R, sizeof(R));
+    detail::iw_and_inverse(R, Ib, Iw_, Iwinv_);
     for (int leg = 0; leg < MPCQP_NUM_LEG; ++leg)
       for (int r = 0; r < 3; ++r) pending_feet_[3 * leg + r] = foot_pos(r, leg);
+    detail::b_mat_c(robot_mass, Iwinv_, pending_feet_, B_mat_c);
   }
 
-  // ConvexMpc.cpp:145-156; also commits the step's B_d into the horizon (the caller's
-  // `B_mat_d_list.block<13,12>(i*13,0) = B_mat_d` line, A1RobotControl.cpp:513).
+  // ConvexMpc.cpp:145-156 (forward Euler).  Remembers the feet behind this call's B_mat_d so that
+  // calculate_qp_mats can recognise the block the caller stores from it.
   void state_space_discretization(double dt) {
     rec_[MPCQP_REC_DT] = dt;
-    if (step_ < N) {
-      std::memcpy(&rec_[MPCQP_REC_FEET(N) + 12 * step_], pending_feet_, sizeof(pending_feet_));
-      ++step_;
-    }
+    for (int i = 0; i < 13; ++i)
+      for (int j = 0; j < 13; ++j) A_mat_d(i, j) = (i == j ? 1.0 : 0.0) + A_mat_c(i, j) * dt;
+    for (int i = 0; i < 13; ++i)
+      for (int j = 0; j < 12; ++j) B_mat_d(i, j) = B_mat_c(i, j) * dt;
+    if (step_ < N) std::memcpy(seen_feet_[step_], pending_feet_, sizeof(pending_feet_));
+    if (step_ < N) std::memcpy(seen_bd_[step_].a, B_mat_d.a, sizeof(B_mat_d.a));
+    ++step_;
   }
 
   // ConvexMpc.cpp:158-245.  State needs mpc_states (13), mpc_states_d (13N) and contacts[4].
   template <class State>
   void calculate_qp_mats(const State& state) {
-    for (int i = step_; i < N; ++i)  // steps never discretized reuse the last feet
-      std::memcpy(&rec_[MPCQP_REC_FEET(N) + 12 * i], pending_feet_, sizeof(pending_feet_));
+    for (int i = 0; i < N; ++i) feet_of_block(i, &rec_[MPCQP_REC_FEET(N) + 12 * i]);
     for (int k = 0; k < MPCQP_STATE_DIM; ++k) rec_[MPCQP_REC_X0 + k] = state.mpc_states[k];
     for (int k = 0; k < MPCQP_STATE_DIM * N; ++k) rec_[MPCQP_REC_XREF + k] = state.mpc_states_d[k];
     for (int l = 0; l < MPCQP_NUM_LEG; ++l) rec_[MPCQP_REC_CONTACTS + l] = state.contacts[l] ? 1.0 : 0.0;
@@ -111,6 +323,7 @@ class ConvexMpc {
     rec_[MPCQP_REC_FZMIN] = fz_min;
     rec_[MPCQP_REC_FZMAX] = fz_max;
     build_on_device();
+    std::fill(linear_constraints.begin(), linear_constraints.end(), 0.0);
     for (int f = 0; f < MPCQP_NUM_LEG * N; ++f) {  // ConvexMpc.cpp:46-58
       double* A = linear_constraints.data();
       A[(size_t)(5 * f + 0) * n + 3 * f + 0] = 1;
@@ -127,70 +340,89 @@ class ConvexMpc {
 
   // the record handed to the solve path (inputs of calculate_qp_mats + the solve)
   const std::vector<double>& record() const { return rec_; }
-  mpcqp_handle* handle() const { return h_; }
+  mpcqp_handle* handle() const { return slot_->h; }
+  int device() const { return device_; }
+  // device staging of the formulation (tests check it lives on device())
+  const double* staging() const { return slot_->d_P; }
 
   double mu, fz_min, fz_max;
+  Mat<13, 13> A_mat_c, A_mat_d;
+  Mat<13, 12> B_mat_c, B_mat_d;
+  Mat<13 * N, 12> B_mat_d_list;            // block i: B_d of horizon step i (written by the caller)
   std::vector<double> hessian;             // dense row-major n x n (reference: sparseView of it)
   std::vector<double> gradient;            // n
   std::vector<double> lb, ub;              // m
   std::vector<double> linear_constraints;  // dense row-major m x n
 
  private:
+  // Feet of horizon step i from B_mat_d_list block i.  The block the reference's loop stores is the
+  // B_mat_d of one of this object's discretizations: its feet are taken as they were given.  Any
+  // other block with the physical structure (rows 0-5, 12 zero; rows 9-11 dt/m I; rows 6-8
+  // I_w^-1 [r]x dt) gives its feet back through I_w; anything else is rejected.
+  void feet_of_block(int i, double* feet) const {
+    const Mat<13, 12> blk = B_mat_d_list.template block<13, 12>(13 * i, 0);
+    for (int s = 0; s < step_ && s < N; ++s)
+      if (!std::memcmp(blk.a, seen_bd_[s].a, sizeof(blk.a))) {
+        std::memcpy(feet, seen_feet_[s], sizeof(seen_feet_[s]));
+        return;
+      }
+    const double dt = rec_[MPCQP_REC_DT], dtm = (1.0 / rec_[MPCQP_REC_MASS]) * dt;
+    bool ok = have_body_ && dt > 0;
+    for (int r = 0; r < 13 && ok; ++r)
+      for (int c = 0; c < 12 && ok; ++c) {
+        const double v = blk(r, c);
+        if (r < 6 || r == 12) ok = v == 0.0;
+        else if (r >= 9) ok = std::fabs(v - (c % 3 == r - 9 ? dtm : 0.0)) <= 1e-12 * dtm;
+      }
+    if (!ok)
+      throw std::invalid_argument("ConvexMpc: B_mat_d_list block " + std::to_string(i) +
+                                  " is not a single-rigid-body B_d of this robot");
+    for (int l = 0; l < MPCQP_NUM_LEG; ++l) {  // [r]x = I_w B_d[6:9, 3l:3l+3] / dt
+      double S[9];
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+          double s = 0.0;
+          for (int k = 0; k < 3; ++k) s += Iw_[3 * a + k] * blk(6 + k, 3 * l + b);
+          S[3 * a + b] = s / dt;
+        }
+      feet[3 * l + 0] = 0.5 * (S[7] - S[5]);
+      feet[3 * l + 1] = 0.5 * (S[2] - S[6]);
+      feet[3 * l + 2] = 0.5 * (S[3] - S[1]);
+    }
+  }
   void build_on_device();
-  void free_device();
-  mpcqp_params params_{};
-  mpcqp_handle* h_ = nullptr;
-  // device staging of build_on_device, allocated on first use and owned by the object
-  double *d_rec_ = nullptr, *d_P_ = nullptr, *d_q_ = nullptr, *d_l_ = nullptr, *d_u_ = nullptr;
+
+  int device_ = 0;
+  detail::BuildSlot<N>* slot_ = nullptr;
   std::vector<double> rec_;
   double pending_feet_[12] = {0};
+  double seen_feet_[N][12] = {};
+  Mat<13, 12> seen_bd_[N];
+  double Iw_[9] = {0}, Iwinv_[9] = {0};
+  bool have_body_ = false;
   int step_ = 0;
 };
 
-}  // namespace mpcqp_cpp
-
-#include <hip/hip_runtime_api.h>
-
-namespace mpcqp_cpp {
-
-template <int N>
-void ConvexMpc<N>::free_device() {
-  (void)hipFree(d_rec_);
-  (void)hipFree(d_P_);
-  (void)hipFree(d_q_);
-  (void)hipFree(d_l_);
-  (void)hipFree(d_u_);
-  d_rec_ = d_P_ = d_q_ = d_l_ = d_u_ = nullptr;
-}
-
 template <int N>
 void ConvexMpc<N>::build_on_device() {
-  auto ok = [&](hipError_t e) {
-    if (e != hipSuccess) throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e));
-  };
-  if (!d_u_) {  // first call: all five buffers or none (a failed allocation frees the others)
-    try {
-      ok(hipMalloc(&d_rec_, sizeof(double) * rec_.size()));
-      ok(hipMalloc(&d_P_, sizeof(double) * hessian.size()));
-      ok(hipMalloc(&d_q_, sizeof(double) * n));
-      ok(hipMalloc(&d_l_, sizeof(double) * m));
-      ok(hipMalloc(&d_u_, sizeof(double) * m));
-    } catch (...) {
-      free_device();
-      throw;
-    }
-  }
-  ok(hipMemcpy(d_rec_, rec_.data(), sizeof(double) * rec_.size(), hipMemcpyHostToDevice));
-  throw_on(mpcqp_build_qp_device(h_, d_rec_, 1, d_P_, d_q_, d_l_, d_u_, nullptr), h_, "mpcqp_build_qp_device");
-  ok(hipMemcpy(hessian.data(), d_P_, sizeof(double) * hessian.size(), hipMemcpyDeviceToHost));
-  ok(hipMemcpy(gradient.data(), d_q_, sizeof(double) * n, hipMemcpyDeviceToHost));
-  ok(hipMemcpy(lb.data(), d_l_, sizeof(double) * m, hipMemcpyDeviceToHost));
-  ok(hipMemcpy(ub.data(), d_u_, sizeof(double) * m, hipMemcpyDeviceToHost));
+  detail::BuildSlot<N>& s = *slot_;
+  std::lock_guard<std::mutex> lk(s.mu);
+  DeviceScope ds(s.device);
+  hip_ok(hipMemcpy(s.d_rec, rec_.data(), sizeof(double) * rec_.size(), hipMemcpyHostToDevice), "hipMemcpy");
+  throw_on(mpcqp_build_qp_device(s.h, s.d_rec, 1, s.d_P, s.d_q, s.d_l, s.d_u, nullptr), s.h, "mpcqp_build_qp_device");
+  hip_ok(hipMemcpy(hessian.data(), s.d_P, sizeof(double) * hessian.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+  hip_ok(hipMemcpy(gradient.data(), s.d_q, sizeof(double) * n, hipMemcpyDeviceToHost), "hipMemcpy");
+  hip_ok(hipMemcpy(lb.data(), s.d_l, sizeof(double) * m, hipMemcpyDeviceToHost), "hipMemcpy");
+  hip_ok(hipMemcpy(ub.data(), s.d_u, sizeof(double) * m, hipMemcpyDeviceToHost), "hipMemcpy");
 }
 
 // ---------------------------------------------------------------------------------------------
-// compute_grf: the MPC branch of A1RobotControl::compute_grf, batched.  Inertia accessor is the
-// only difference between A1CtrlStates (a1_trunk_inertia) and Go1CtrlStates (go1_trunk_inertia).
+// compute_grf: the MPC branch of A1RobotControl::compute_grf, batched.  Like the reference's
+// controller (A1RobotControl.h:67 member OsqpEigen::Solver, setWarmStart(true) at
+// A1RobotControl.cpp:524) it owns a persistent solver: one device warm-start slot per robot, the
+// first tick an initSolver, later ticks update + warm solve (mpcqp_solve_batch_warm_host).  Inertia
+// accessor is the only difference between A1CtrlStates (a1_trunk_inertia) and Go1CtrlStates
+// (go1_trunk_inertia).
 // ---------------------------------------------------------------------------------------------
 struct A1InertiaOf {
   template <class S> static const auto& get(const S& s) { return s.a1_trunk_inertia; }
@@ -203,13 +435,19 @@ template <class InertiaOf, int N = 10>
 class RobotControlT {
  public:
   template <class VecQ, class VecR>
-  RobotControlT(const VecQ& q_weights, const VecR& r_weights, int device = 0) {
+  RobotControlT(const VecQ& q_weights, const VecR& r_weights, int device = 0) : device_(device) {
     mpcqp_default_params(&params_, N);
     for (int i = 0; i < MPCQP_STATE_DIM; ++i) params_.q_weights[i] = q_weights[i];
     for (int i = 0; i < MPCQP_NUM_DOF; ++i) params_.r_weights[i] = r_weights[i];
     throw_on(mpcqp_create(&params_, device, &h_), nullptr, "mpcqp_create");
   }
-  ~RobotControlT() { if (h_) mpcqp_destroy(h_); }
+  ~RobotControlT() {
+    if (d_state_) {
+      DeviceScope ds(device_);
+      (void)hipFree(d_state_);
+    }
+    if (h_) mpcqp_destroy(h_);
+  }
   RobotControlT(const RobotControlT&) = delete;
   RobotControlT& operator=(const RobotControlT&) = delete;
 
@@ -217,6 +455,9 @@ class RobotControlT {
   // The reference's ROS param `use_sim_time` (read at A1RobotControl.cpp:63): when true, the MPC
   // horizon uses the caller's dt instead of mpc_dt (:464-467).
   bool use_sim_time = false;
+  // Persistent warm-started solver per robot (production, A1RobotControl.cpp:524).  false: every
+  // call is a fresh cold solve (test_mpc.cpp:131-133).
+  bool warm_start = true;
   double mu = 0.3, fz_min = 0.0, fz_max = 180.0;
 
   // A1RobotControl.cpp:452-514: mutates state.mpc_states / mpc_states_d / root_lin_vel_d_world
@@ -277,14 +518,23 @@ class RobotControlT {
 
   // Batched compute_grf: forces[b] receives foot_forces_grf (3x4, row r / leg l at [r*4+l]).
   // `dt` is the caller's thread period; it is the horizon step only when use_sim_time is set.
+  // Robot b keeps warm-start slot b from call to call (a change of `count` re-initialises all).
   template <class State>
   void compute_grf_batch(State* states, int count, double* forces, mpcqp_result* results = nullptr,
                          double dt = 0.0) {
+    if (use_sim_time && !(std::isfinite(dt) && dt > 0.0))
+      throw std::invalid_argument("compute_grf: use_sim_time needs the caller's dt (finite, > 0)");
     const double hdt = use_sim_time ? dt : mpc_dt;  // A1RobotControl.cpp:462-467
     recs_.resize((size_t)count * MPCQP_REC_SIZE(N));
     res_.resize(count);
     for (int b = 0; b < count; ++b) assemble(states[b], &recs_[(size_t)b * MPCQP_REC_SIZE(N)], hdt);
-    throw_on(mpcqp_solve_batch_host(h_, recs_.data(), count, res_.data(), nullptr), h_, "mpcqp_solve_batch_host");
+    if (warm_start) {
+      ensure_slots(count);
+      throw_on(mpcqp_solve_batch_warm_host(h_, recs_.data(), count, d_state_, res_.data(), nullptr), h_,
+               "mpcqp_solve_batch_warm_host");
+    } else {
+      throw_on(mpcqp_solve_batch_host(h_, recs_.data(), count, res_.data(), nullptr), h_, "mpcqp_solve_batch_host");
+    }
     for (int b = 0; b < count; ++b) {
       for (int l = 0; l < 4; ++l)
         for (int r = 0; r < 3; ++r) forces[(size_t)b * 12 + r * 4 + l] = res_[b].f_body[3 * l + r];
@@ -292,14 +542,34 @@ class RobotControlT {
     }
   }
 
-  // A1RobotControl::compute_grf(state, dt) — single robot; like the reference, the horizon step is
-  // mpc_dt = 0.0025 on hardware and `dt` when use_sim_time is set (:458-467).
-  template <class State, class Mat34>
-  void compute_grf(State& state, double dt, Mat34& foot_forces_grf) {
+  // A1RobotControl::compute_grf(A1CtrlStates& state, double dt) -> Eigen::Matrix<double,3,NUM_LEG>
+  // (A1RobotControl.h:44): single robot, warm-started from this controller's previous call.  Like
+  // the reference, the horizon step is mpc_dt = 0.0025 and `dt` only with use_sim_time (:458-467).
+  // A leg whose solution norm is NaN keeps a zero column (the reference leaves it uninitialised).
+  template <class State>
+  Matrix34 compute_grf(State& state, double dt) {
     double f[12];
     compute_grf_batch(&state, 1, f, nullptr, dt);
+    Matrix34 out;
     for (int r = 0; r < 3; ++r)
-      for (int l = 0; l < 4; ++l) foot_forces_grf(r, l) = f[r * 4 + l];
+      for (int l = 0; l < 4; ++l) out(r, l) = f[r * 4 + l];
+    return out;
+  }
+  // out-parameter form of the same call
+  template <class State, class Mat34>
+  void compute_grf(State& state, double dt, Mat34& foot_forces_grf) {
+    const Matrix34 f = compute_grf(state, dt);
+    for (int r = 0; r < 3; ++r)
+      for (int l = 0; l < 4; ++l) foot_forces_grf(r, l) = f(r, l);
+  }
+  // status / iterations / residuals of the last compute_grf call (robot b of a batch)
+  const mpcqp_result& last_result(int b = 0) const { return res_.at(b); }
+  // forget the warm-start state (the next call is an initSolver again)
+  void reset_warm_start() {
+    if (d_state_) {
+      DeviceScope ds(device_);
+      hip_ok(hipMemset(d_state_, 0, sizeof(double) * slot_doubles() * slots_), "hipMemset");
+    }
   }
 
   // ---- stance_leg_control_type == 0: single-step QP balance controller -----------------------
@@ -365,10 +635,27 @@ class RobotControlT {
   }
 
   mpcqp_handle* handle() const { return h_; }
+  int device() const { return device_; }
+  const double* warm_slots() const { return d_state_; }
 
  private:
+  static size_t slot_doubles() { return (size_t)mpcqp_warm_state_size(N); }
+  void ensure_slots(int count) {
+    if (count == slots_ && d_state_) return;
+    DeviceScope ds(device_);
+    if (d_state_) hip_ok(hipFree(d_state_), "hipFree");
+    d_state_ = nullptr;
+    slots_ = 0;
+    hip_ok(hipMalloc(&d_state_, sizeof(double) * slot_doubles() * count), "hipMalloc");
+    hip_ok(hipMemset(d_state_, 0, sizeof(double) * slot_doubles() * count), "hipMemset");  // = not initialised
+    slots_ = count;
+  }
+
   mpcqp_params params_{};
   mpcqp_handle* h_ = nullptr;
+  int device_ = 0;
+  double* d_state_ = nullptr;
+  int slots_ = 0;
   std::vector<double> recs_;
   std::vector<double> bal_recs_;
   std::vector<mpcqp_result> res_;

@@ -13,7 +13,7 @@ struct Vec {  // Eigen::VectorXd stand-in for the test (operator[])
   double& operator[](int i) { return v[i]; }
   const double& operator[](int i) const { return v[i]; }
 };
-struct Mat {  // Eigen::Matrix stand-in (operator()(r,c)), row-major up to 3x4
+struct Mat {  // Eigen::Matrix<double,3,4> / Matrix3d stand-in (operator()(r,c)), row-major up to 3x4
   double a[3][4] = {{0}};
   double& operator()(int r, int c) { return a[r][c]; }
   const double& operator()(int r, int c) const { return a[r][c]; }
@@ -83,6 +83,7 @@ int main() {
     for (int l = 0; l < 4; ++l)
       for (int r = 0; r < 3; ++r) state.foot_pos_abs_mpc(r, l) -= state.root_lin_vel_d[r] * dt;
     mpc_solver.state_space_discretization(dt);
+    mpc_solver.B_mat_d_list.block<13, 12>(i * 13, 0) = mpc_solver.B_mat_d;  // :121, verbatim
   }
   mpc_solver.calculate_qp_mats(state);  // :125
   double hsum = 0, hmax = 0, gsum = 0;
@@ -103,21 +104,50 @@ int main() {
     std::printf("\n");
   }
 
-  // compute_grf (A1RobotControl.cpp:446-561) on the same stance, production assembly
+  // the formulation's device staging lives on the handle's device
+  hipPointerAttribute_t at;
+  mpcqp_cpp::hip_ok(hipPointerGetAttributes(&at, mpc_solver.staging()), "hipPointerGetAttributes");
+  std::printf("STAGING_DEVICE %d HANDLE_DEVICE %d\n", at.device, mpc_solver.device());
+
+  // B_mat_d_list is an input: a block the caller computed elsewhere (here: feet of step 3 moved by
+  // +0.01 in x through a second ConvexMpc) is read back into the formulation through I_w.
+  {
+    mpcqp_cpp::ConvexMpc<PLAN_HORIZON> other(q_weights, r_weights);
+    Mat moved = state.foot_pos_rel;
+    for (int l = 0; l < 4; ++l)
+      for (int r = 0; r < 3; ++r) moved(r, l) -= 3 * state.root_lin_vel_d[r] * dt;
+    for (int l = 0; l < 4; ++l) moved(0, l) += 0.01;
+    other.calculate_A_mat_c(avg);
+    other.calculate_B_mat_c(state.robot_mass, state.a1_trunk_inertia, state.root_rot_mat, moved);
+    other.state_space_discretization(dt);
+    mpc_solver.B_mat_d_list.block<13, 12>(3 * 13, 0) = other.B_mat_d;
+    mpc_solver.calculate_qp_mats(state);
+    std::printf("RECOVERED_FEET");
+    for (int k = 0; k < 12; ++k) std::printf(" %.17g", mpc_solver.record()[MPCQP_REC_FEET(PLAN_HORIZON) + 36 + k]);
+    double hs = 0;
+    for (double v : mpc_solver.hessian) hs += v;
+    std::printf("\nRECOVERED_HESSIAN_SUM %.17g\n", hs);
+    std::printf("RECORD");
+    for (double v : mpc_solver.record()) std::printf(" %.17g", v);
+    std::printf("\n");
+  }
+
+  // compute_grf (A1RobotControl.h:44, A1RobotControl.cpp:446-561) on the same stance, production
+  // assembly: `foot_forces_grf = compute_grf(state, dt)` with the 3x4 return value
   state.foot_pos_abs = state.foot_pos_rel;
   state.root_pos_d[2] = 0.15;
   mpcqp_cpp::A1RobotControl ctrl(q_weights, r_weights);
-  Mat forces;
-  ctrl.compute_grf(state, dt, forces);
+  Mat forces = ctrl.compute_grf(state, dt);
   for (int r = 0; r < 3; ++r) {
     std::printf("GRF");
     for (int l = 0; l < 4; ++l) std::printf(" %.17g", forces(r, l));
     std::printf("\n");
   }
   // Gazebo: use_sim_time makes the horizon step the caller's dt (A1RobotControl.cpp:464-467)
-  ctrl.use_sim_time = true;
+  mpcqp_cpp::A1RobotControl ctrl_sim(q_weights, r_weights);
+  ctrl_sim.use_sim_time = true;
   Mat forces_sim;
-  ctrl.compute_grf(state, 0.004, forces_sim);
+  ctrl_sim.compute_grf(state, 0.004, forces_sim);
   for (int r = 0; r < 3; ++r) {
     std::printf("GRFSIM");
     for (int l = 0; l < 4; ++l) std::printf(" %.17g", forces_sim(r, l));

@@ -7,7 +7,8 @@ validated before it is written:
     of ConvexMpc) to 1e-13 relative;
   * the converged solution (eps 1e-9) against an independent dense primal-dual interior-point
     solve of the same QP (objective within 1e-5 relative, constraint violation <= 1e-6).
-Run:  python tests/golden/make_golden.py
+Run:  python tests/golden/make_golden.py        (every set)
+      python tests/golden/make_golden.py r03    (the horizon-20 and interval-100 sets only)
 """
 import os
 import sys
@@ -23,8 +24,8 @@ import numpy_reference as nr  # noqa: E402
 from mpcqp import records  # noqa: E402  (host record assembly; pure numpy, no GPU)
 
 
-def make_set(name, recs, q, r, N=10):
-    p = po.default_params(N, q=list(q), r=list(r))
+def make_set(name, recs, q, r, N=10, interval=25):
+    p = po.default_params(N, q=list(q), r=list(r), adaptive_rho_interval=interval)
     pc = po.default_params(N, q=list(q), r=list(r), eps_abs=1e-9, eps_rel=1e-9, max_iter=50000)
     B = recs.shape[0]
     res, sol = po.solve_batch(p, recs, nthreads=8, want_solution=True)
@@ -37,7 +38,9 @@ def make_set(name, recs, q, r, N=10):
         assert np.max(np.abs(g - g2)) <= 1e-13 * max(np.max(np.abs(g2)), 1e-300) + 1e-300, (name, b)
         assert np.array_equal(A, C2) and np.array_equal(l, l2) and np.array_equal(u, u2)
         # independent certificate: a dense primal-dual interior-point solve of the same QP
-        xi = nr.ipm_qp(H2, g2, C2, l2, u2)
+        # (at N = 20, cond(H) ~ 2.5e6: the IPM's own stop at 1e-10 lands on a worse point through
+        # roundoff in its reduced KKT solve; 1e-9 is where it agrees with the OSQP restatement)
+        xi = nr.ipm_qp(H2, g2, C2, l2, u2, tol=1e-10 if N <= 10 else 1e-9)
         f = lambda x: 0.5 * x @ H2 @ x + g2 @ x  # noqa: E731
         fscale = np.abs(g2) @ np.abs(xi) + 0.5 * np.abs(xi) @ np.abs(H2) @ np.abs(xi) + 1e-300
         assert abs(f(solc[b]) - f(xi)) <= 1e-5 * fscale + 1e-8, (name, b, f(solc[b]), f(xi))
@@ -50,12 +53,14 @@ def make_set(name, recs, q, r, N=10):
                         u0=res["u0"], f_body=res["f_body"], x=sol, status=res["status"],
                         iters=res["iters"], rho_updates=res["rho_updates"], obj_val=res["obj_val"],
                         x_converged=solc, status_converged=resc["status"],
-                        hessian_sum=hsum, gradient_sum=gsum)
+                        hessian_sum=hsum, gradient_sum=gsum, horizon=N, adaptive_rho_interval=interval)
     print(f"{out}: {B} instances, iters {res['iters'].min()}..{res['iters'].max()}, "
           f"status {np.unique(res['status'])}")
 
 
-def main():
+def main(only=None):
+    if only == "r03":
+        return main_r03()
     rec, q, r = records.assemble_test_mpc(10)
     make_set("test_mpc", rec[None], q, r)
     st = records.synthetic_go1(32, seed=1001, gait="trot")
@@ -76,7 +81,25 @@ def main():
     st = records.synthetic_go1(16, seed=9001, gait="trot")
     st.robot_mass = np.full(16, 12.0)
     make_set("gazebo_weights", records.assemble_compute_grf(st, 10), qg, rg)
+    main_r03()
+
+
+def main_r03():
+    """Round-3 sets: horizon 20 (config C4) and OSQP 0.6's non-profiling adaptive-rho interval."""
+    rec, q, r = records.assemble_test_mpc(20)
+    make_set("test_mpc_n20", rec[None], q, r, N=20)
+    st = records.synthetic_go1(16, seed=2001, gait="trot")
+    make_set("go1_trot_n20", records.assemble_compute_grf(st, 20), records.GO1_Q, records.GO1_R, N=20)
+    st = records.synthetic_go1(16, seed=2002, gait="mixed", mixed_mu=True)
+    make_set("go1_mixed_n20", records.assemble_compute_grf(st, 20), records.GO1_Q, records.GO1_R, N=20)
+    # OSQP 0.6 built without profiling: adaptive_rho_interval = 4 x check_termination = 100
+    st = records.synthetic_go1(32, seed=1001, gait="trot")
+    make_set("go1_trot_interval100", records.assemble_compute_grf(st, 10), records.GO1_Q, records.GO1_R,
+             interval=100)
+    st = records.synthetic_go1(32, seed=5001, gait="mixed", mixed_mu=True)
+    make_set("go1_mixed_interval100", records.assemble_compute_grf(st, 10), records.GO1_Q, records.GO1_R,
+             interval=100)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

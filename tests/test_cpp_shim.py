@@ -21,7 +21,11 @@ def test_cpp_test_mpc_harness(oracle):
     rows, grf, grf_sim = [], [], []
     for line in out.splitlines():
         parts = line.split()
-        if parts[0] == "ROW":
+        if parts[0] in ("RECOVERED_FEET", "RECORD"):
+            kv[parts[0]] = np.array([float(x) for x in parts[1:]])
+        elif parts[0] == "STAGING_DEVICE":
+            kv["staging_device"], kv["handle_device"] = int(parts[1]), int(parts[3])
+        elif parts[0] == "ROW":
             rows.append([float(x) for x in parts[1:]])
         elif parts[0] == "GRF":
             grf.append([float(x) for x in parts[1:]])
@@ -41,6 +45,16 @@ def test_cpp_test_mpc_harness(oracle):
     u0 = np.array(rows).T.reshape(12)  # [leg][xyz]
     assert np.max(np.abs(u0 - ref["u0"])) <= 1e-4 * max(np.max(np.abs(ref["u0"])), 1)
     assert (kv["status"], kv["iters"], kv["rho_updates"]) == (int(ref["status"]), int(ref["iters"]), int(ref["rho_updates"]))
+    # the formulation's device staging is on the handle's device
+    assert kv["staging_device"] == kv["handle_device"]
+    # B_mat_d_list block 3 replaced by a B_d of feet moved +0.01 in x: read back through I_w
+    feet3 = rec[mpcqp.rec_feet(10) + 36: mpcqp.rec_feet(10) + 48].reshape(4, 3).copy()
+    feet3[:, 0] += 0.01
+    np.testing.assert_allclose(kv["RECOVERED_FEET"].reshape(4, 3), feet3, rtol=0, atol=1e-12)
+    rec_mod = kv["RECORD"]
+    P2, _, _, _, _ = oracle.build_qp(op, rec_mod)
+    assert abs(kv["RECOVERED_HESSIAN_SUM"] - P2.sum()) <= 1e-12 * np.abs(P2).sum()
+    assert abs(P2.sum() - P.sum()) > 1e-9 * np.abs(P).sum()  # the moved feet changed H
     # compute_grf (production assembly) on the same stance
     s = oracle.RobotState()
     s.root_pos[:] = [0, 0, 0.15]
@@ -86,3 +100,49 @@ def test_cpp_balance_branch(oracle):
     fr = np.array(ref["f_body"]).reshape(4, 3).T
     np.testing.assert_array_equal(np.array(grf), fr)
     assert fr[2, 0] > 20 and fr[2, 3] > 20 and np.all(np.abs(fr[:, 1:3]) < 0.05)  # swing legs: 0 within OSQP eps
+
+
+@pytest.mark.gpu
+def test_cpp_warm_ticks_match_oracle_sequence(oracle, tmp_path):
+    """24 production ticks through the C++ drop-in: per-robot controllers calling
+    `foot_forces_grf = compute_grf(state, dt)` (persistent warm-started solver, A1RobotControl.h:67)
+    and one batched controller, against the oracle's persistent solver tick by tick (ws_update:
+    initSolver, then update_P / re-init and a warm solve): status, iterations, u0 within 1e-4."""
+    exe = os.path.join(REPO, "tests", "cpp", "build", "test_warm_ticks_gpu")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(REPO, "tests", "cpp")], check=True)
+    T, B = 24, 6
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=41, gait="trot", swing_ticks=5)
+    rows = np.stack([mpcqp.pack_states(st) for st in ticks])  # [T][B][ST_SIZE]
+    path = tmp_path / "states.bin"
+    np.ascontiguousarray(rows, dtype=np.float64).tofile(path)
+    out = subprocess.run([exe, str(path), str(T), str(B)], check=True, capture_output=True, text=True,
+                         timeout=120).stdout
+    got = {"TICK": {}, "BATCH": {}}
+    grf = {}
+    for line in out.splitlines():
+        p = line.split()
+        if p[0] in got:
+            got[p[0]][(int(p[1]), int(p[2]))] = (int(p[3]), int(p[4]), int(p[5]), np.array([float(x) for x in p[6:]]))
+        elif p[0] == "GRF":
+            grf[(int(p[1]), int(p[2]))] = np.array([float(x) for x in p[3:]]).reshape(3, 4)
+    recs_t = np.stack([mpcqp.assemble_compute_grf(st, 10) for st in ticks])
+    ref = oracle.solve_sequence(oracle.default_params(10), recs_t, nthreads=4)
+    warm_iters = []
+    for tag in ("TICK", "BATCH"):
+        assert len(got[tag]) == T * B, tag
+        for t in range(T):
+            for b in range(B):
+                st, it, ru, u0 = got[tag][(t, b)]
+                r = ref[t][b]
+                assert st == int(r["status"]), (tag, t, b)
+                assert it == int(r["iters"]), (tag, t, b, it, int(r["iters"]))
+                err = np.max(np.abs(u0 - r["u0"])) / max(np.max(np.abs(r["u0"])), 1.0)
+                assert err <= 1e-4, (tag, t, b, err)
+                if tag == "TICK":
+                    warm_iters.append(it if t else None)
+                    fb = np.array(r["f_body"]).reshape(4, 3).T
+                    assert np.max(np.abs(grf[(t, b)] - fb)) <= 1e-4 * max(np.max(np.abs(fb)), 1.0)
+    cold = oracle.solve_batch(oracle.default_params(10), recs_t[1:].reshape(-1, recs_t.shape[-1]), nthreads=4)
+    warm = np.array([w for w in warm_iters if w is not None])
+    assert warm.mean() < 0.6 * cold["iters"].mean()  # the warm start is really in effect

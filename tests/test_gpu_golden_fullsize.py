@@ -18,7 +18,9 @@ SETS = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endsw
 @pytest.mark.parametrize("path", SETS, ids=[os.path.basename(p) for p in SETS])
 def test_gpu_matches_golden(path):
     d = np.load(path)
-    p = mpcqp.default_params(10, q_weights=d["q_weights"], r_weights=d["r_weights"])
+    N = int(d["horizon"]) if "horizon" in d else 10
+    interval = int(d["adaptive_rho_interval"]) if "adaptive_rho_interval" in d else 25
+    p = mpcqp.default_params(N, q_weights=d["q_weights"], r_weights=d["r_weights"], adaptive_rho_interval=interval)
     with mpcqp.MpcQpSolver(p) as s:
         got, sol, _ = solve_gpu(s, d["records"])
     assert np.all(rel_err_u0(got["u0"], d["u0"]) <= 1e-4)
@@ -29,11 +31,11 @@ def test_gpu_matches_golden(path):
     assert np.all(full <= 1e-4)
 
 
-def _pyramid_violation(recs, sol):
+def _pyramid_violation(recs, sol, N=10):
     """max over rows of dist(Ax, [l, u]) per robot (friction pyramid + fz bounds)."""
     B = recs.shape[0]
     mu = recs[:, mpcqp._lib.REC_MU][:, None]
-    c = np.tile(recs[:, mpcqp._lib.REC_CONTACTS:mpcqp._lib.REC_CONTACTS + 4] != 0, (1, 10))
+    c = np.tile(recs[:, mpcqp._lib.REC_CONTACTS:mpcqp._lib.REC_CONTACTS + 4] != 0, (1, N))
     x = sol.reshape(B, -1, 3)
     fx, fy, fz = x[..., 0], x[..., 1], x[..., 2]
     v = np.stack([-(fx + mu * fz), fx - mu * fz, -(fy + mu * fz), fy - mu * fz, -fz, fz - 180 * c])
@@ -81,3 +83,40 @@ def test_batch_order_independence():
         c, sc, _ = solve_gpu(s, recs[:1])
     np.testing.assert_array_equal(sa[perm], sb)
     np.testing.assert_array_equal(sa[:1], sc)
+
+
+def test_c4_fullsize_properties(oracle):
+    """Config C4 at its full size: 4096 trot robots at horizon 20 (n = 240, m = 400).  Every robot
+    solved, deterministic on a re-run, friction pyramid within the robot's primal residual, and a
+    96-robot subset schedule-identical with the oracle."""
+    B, N = 4096, 20
+    st = mpcqp.synthetic_go1(B, seed=3000, gait="trot")
+    recs = mpcqp.assemble_compute_grf(st, N)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(N)) as s:
+        got, sol, _ = solve_gpu(s, recs)
+        got2, sol2, _ = solve_gpu(s, recs)
+    np.testing.assert_array_equal(sol, sol2)
+    np.testing.assert_array_equal(got["iters"], got2["iters"])
+    assert np.all(got["status"] == mpcqp._lib.STATUS_SOLVED)
+    assert np.all(_pyramid_violation(recs, sol, N) <= got["pri_res"] + 1e-9)
+    idx = np.random.default_rng(3).choice(B, 96, replace=False)
+    ref = oracle.solve_batch(oracle.default_params(N), recs[idx], nthreads=8)
+    assert np.all(rel_err_u0(got["u0"][idx], ref["u0"]) <= 1e-4)
+    np.testing.assert_array_equal(got["status"][idx], ref["status"])
+    assert np.mean(got["iters"][idx] == ref["iters"]) >= 0.95
+
+
+@pytest.mark.parametrize("gait", ["trot", "mixed"])
+def test_interval100_schedule_on_gpu(oracle, gait):
+    """OSQP 0.6's adaptive-rho interval without profiling (4 x check_termination = 100) on the
+    device vs the oracle at the same interval, on a fresh 256-robot batch."""
+    st = mpcqp.synthetic_go1(256, seed=4100, gait=gait, mixed_mu=(gait == "mixed"))
+    recs = mpcqp.assemble_compute_grf(st, 10)
+    p = mpcqp.default_params(10, adaptive_rho_interval=100)
+    with mpcqp.MpcQpSolver(p) as s:
+        got, _, _ = solve_gpu(s, recs)
+    ref = oracle.solve_batch(oracle.default_params(10, adaptive_rho_interval=100), recs, nthreads=8)
+    assert np.all(rel_err_u0(got["u0"], ref["u0"]) <= 1e-4)
+    np.testing.assert_array_equal(got["status"], ref["status"])
+    np.testing.assert_array_equal(got["iters"], ref["iters"])
+    np.testing.assert_array_equal(got["rho_updates"], ref["rho_updates"])

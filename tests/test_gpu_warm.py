@@ -120,3 +120,27 @@ def test_warm_mu_change_reinit(oracle):
     fz = u[:, :, 2]
     tol = 0.25  # OSQP primal tolerance (test_oracle.test_solution_respects_friction_pyramid)
     assert np.all(np.abs(u[:, :, :2]).max(-1) <= 0.3 * fz + tol)
+
+
+def test_python_robot_control_is_warm_and_mutates_state(oracle):
+    """mpcqp.RobotControl.compute_grf over consecutive ticks == the oracle's persistent solver, and
+    it writes mpc_states / mpc_states_d / root_lin_vel_d_world like A1RobotControl.cpp:452-488."""
+    T, B, N = 8, 32, 10
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=77, gait="trot", swing_ticks=3)
+    recs_t = np.stack([mpcqp.assemble_compute_grf(s, N) for s in ticks])
+    ref = _oracle_sequence(oracle, mpcqp.default_params(N), recs_t)
+    ctrl = mpcqp.RobotControl()
+    try:
+        for t, st in enumerate(ticks):
+            f = ctrl.compute_grf(st, dt=0.002)
+            got = ctrl.last_results
+            np.testing.assert_array_equal(got["status"], ref[t]["status"])
+            assert np.mean(got["iters"] == ref[t]["iters"]) >= 0.9
+            assert np.all(rel_err_u0(got["u0"], ref[t]["u0"]) <= 1e-4)
+            np.testing.assert_allclose(f, ref[t]["f_body"].reshape(B, 4, 3).transpose(0, 2, 1), atol=1e-4 * 200)
+            np.testing.assert_array_equal(st.mpc_states, recs_t[t][:, :13])
+            np.testing.assert_array_equal(st.mpc_states_d, recs_t[t][:, 44:44 + 13 * N])
+            np.testing.assert_allclose(st.root_lin_vel_d_world,
+                                       np.einsum("bij,bj->bi", st.root_rot_mat, st.root_lin_vel_d))
+    finally:
+        ctrl.close()

@@ -14,15 +14,23 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SETS = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endswith("balance.npz"))
 
 
+def _meta(d):
+    """(horizon, adaptive-rho interval) of a golden set (sets from before round 3: 10, 25)."""
+    return (int(d["horizon"]) if "horizon" in d else 10,
+            int(d["adaptive_rho_interval"]) if "adaptive_rho_interval" in d else 25)
+
+
 def test_golden_sets_present():
     names = {os.path.basename(p)[:-4] for p in SETS}
-    assert {"test_mpc", "go1_trot", "go1_mixed", "edge", "gazebo_weights"} <= names
+    assert {"test_mpc", "go1_trot", "go1_mixed", "edge", "gazebo_weights", "test_mpc_n20", "go1_trot_n20",
+            "go1_mixed_n20", "go1_trot_interval100", "go1_mixed_interval100"} <= names
 
 
 @pytest.mark.parametrize("path", SETS, ids=[os.path.basename(p) for p in SETS])
 def test_oracle_reproduces_golden(oracle, path):
     d = np.load(path)
-    p = oracle.default_params(10, q=list(d["q_weights"]), r=list(d["r_weights"]))
+    N, interval = _meta(d)
+    p = oracle.default_params(N, q=list(d["q_weights"]), r=list(d["r_weights"]), adaptive_rho_interval=interval)
     res, sol = oracle.solve_batch(p, d["records"], nthreads=4, want_solution=True)
     np.testing.assert_array_equal(res["status"], d["status"])
     np.testing.assert_array_equal(res["iters"], d["iters"])
@@ -34,10 +42,11 @@ def test_oracle_reproduces_golden(oracle, path):
 @pytest.mark.parametrize("path", SETS, ids=[os.path.basename(p) for p in SETS])
 def test_formulation_matches_independent_restatement(oracle, path):
     d = np.load(path)
-    p = oracle.default_params(10, q=list(d["q_weights"]), r=list(d["r_weights"]))
+    N, _ = _meta(d)
+    p = oracle.default_params(N, q=list(d["q_weights"]), r=list(d["r_weights"]))
     for b in range(min(4, d["records"].shape[0])):
         P, g, l, u, A = oracle.build_qp(p, d["records"][b])
-        H2, g2, C2, l2, u2 = nr.condensed_qp(d["records"][b], 10, d["q_weights"], d["r_weights"])
+        H2, g2, C2, l2, u2 = nr.condensed_qp(d["records"][b], N, d["q_weights"], d["r_weights"])
         assert np.max(np.abs(P - H2)) <= 1e-13 * np.max(np.abs(H2))
         assert np.max(np.abs(g - g2)) <= 1e-13 * max(np.max(np.abs(g2)), 1e-300) + 1e-300
         np.testing.assert_array_equal(A, C2)
@@ -121,3 +130,13 @@ def test_test_mpc_forces_physical(oracle):
     assert f[0, 2] > 10 and f[2, 2] > 10
     assert np.all(np.abs(f[[1, 3]]) < 1e-3)
     assert d["status"][0] == 1
+
+
+def test_interval100_changes_the_schedule():
+    """The interval-100 sets (OSQP 0.6 without profiling) are not the interval-25 schedule: the
+    same records give different iteration counts for most robots."""
+    a = np.load(os.path.join(GOLDEN, "go1_trot.npz"))
+    b = np.load(os.path.join(GOLDEN, "go1_trot_interval100.npz"))
+    np.testing.assert_array_equal(a["records"], b["records"])
+    assert np.mean(a["iters"] != b["iters"]) > 0.5
+    assert np.all(b["status"] == 1)
