@@ -50,6 +50,9 @@ __device__ __forceinline__ int opaque(int v) {
   asm volatile("" : "+v"(v));
   return v;
 }
+// Pins a value read from LDS into a register: the asm hides where it came from, so the compiler
+// cannot rematerialize it later by reloading LDS that has been reused in between.
+__device__ __forceinline__ void keep(double& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 __device__ __forceinline__ double dabs(double a) { return __builtin_fabs(a); }

@@ -1,0 +1,400 @@
+// mpcqp_schur.h — the KKT solve of wave_kernel for horizons N <= 10 through the problem's
+// velocity-impulse structure (a Woodbury / Schur-complement form with a dense 6N x 6N core),
+// replacing the Riccati chains: every ADMM iteration becomes one dense 6N x 6N mat-vec spread over
+// the 64 lanes plus per-leg 3x3 and per-step 6x12 products, with no sequential horizon recursion.
+// Not installed.
+//
+// Structure (ConvexMpc.cpp:110-211; A_c is nilpotent on the 12 moving states, Ac^2 = 0).  An input
+// u_j enters the state only through its impulse v_j = B_j^(6) u_j on the angular / linear
+// velocities (rows 6-11 of B_d(j): I_w^-1 [r_l]x dt and dt/m I), and
+//   x_{i+1}[6:12] = sum_{j<=i} v_j,   x_{i+1}[0:6] = Ac6 sum_{j<=i} (i - j) v_j,
+// so B'Q̄B = B6' M B6 with B6 = blockdiag(B_j^(6)) (6N x 12N) and the 6N x 6N matrix
+//   M_jl = beta_jl Qv + alpha_jl Ac6' Qp Ac6,  beta_jl = N - max(j,l),
+//   alpha_jl = sum_{i=max(j,l)}^{N-1} (i - j)(i - l),  Qv = diag 2q[6:12], Qp = diag 2q[0:6].
+// OSQP's reduced KKT matrix (scaled) is K = D (c B6'M B6 + R') D with R' = c R + D^-1 (sigma I +
+// A~' diag(rho) A~) D^-1, 3x3 block-diagonal per foot (mpcqp_wave.hip header).  With C = c M,
+// G = B6 R'^-1 B6' = L L' (6x6 blocks per step, Cholesky), Li = L^-1, S = I + L' C L (SPD, all
+// eigenvalues >= 1, condition ~1e0-1e3 on the Go1 workload):
+//   (c B6'M B6 + R')^-1 w = R'^-1 w - B' (I - S^-1) B w,   B := Li B6 R'^-1  (6N x 12N, per step 6x12)
+// (push-through identity; exact in real arithmetic).  Per factorization (rho change): R'^-1 per
+// foot, B (per step), S (6N x 6N) and Q = I - S^-1 by an in-register Gauss-Jordan sweep.  Per ADMM
+// iteration:  z = B w (6x12 per step),  q = Q z (dense, one lane per row of Q),  u = R'^-1 w - B' q.
+//
+// Lane roles inside the one wave of a robot: the ADMM layout of wave_kernel (variable lanes: step
+// 4r + gray(q) of round r in DPP row q, lane 4 leg + a) and, for the dense part, one lane per impulse
+// unknown i = 6 k + c (step k, component c: omega_x,y,z, v_x,y,z), i < 6N <= 60.  The two meet
+// through LDS (w out, q back), in order within the wave.
+#pragma once
+#include "mpcqp_wave_common.h"
+
+namespace mpcqp {
+namespace wv {
+
+template <int N>
+struct SchurCfg {
+  static_assert(N >= 1 && N <= 10, "one lane per impulse unknown: 6N <= 64");
+  static constexpr int NI = 6 * N;  // impulse unknowns
+  // LDS row stride of Q (doubles): rows 528 B apart put lanes i .. i+7 of a ds_read_b128 on eight
+  // distinct 16-B bank groups (a 512-B stride would put all of them on one)
+  static constexpr int QS = 66;
+};
+
+// Factorization scratch: lives in the rows of Q (which every factorization rewrites at its end).
+template <int N>
+struct SchurScratch {
+  static constexpr int NI = SchurCfg<N>::NI;
+  alignas(16) double Rt[N][4][6];   // R'_k foot blocks, upper triangle (00 01 02 11 12 22)
+  alignas(16) double Ri[N][4][9];   // R'^-1 foot blocks, row-major
+  alignas(16) double B6R[NI][12];   // rows of B6 R'^-1 (step k = i / 6)
+  alignas(16) double G[N][36];      // G_k = B_k R'_k^-1 B_k' (row c written by lane 6k + c)
+  alignas(16) double BL[NI][12];    // rows of B = Li B6 R'^-1
+  alignas(16) double VW[NI][12];    // columns of sqrt(c) Qv^1/2 L_k and sqrt(c) Qp^1/2 Ac6 L_k
+};
+
+template <int N>
+struct SchurLds {
+  static constexpr int NI = SchurCfg<N>::NI, QS = SchurCfg<N>::QS;
+  union {
+    alignas(16) double Q[NI][QS];  // I - S^-1, row i in absolute column order; columns NI..63 zero
+    SchurScratch<N> s;
+  };
+  alignas(16) double wv[12 * N + 4];  // w = D^-1 rhs by variable index 12 k + 3 leg + a
+  alignas(16) double qv[64];          // q = Q z by impulse index
+};
+static_assert(sizeof(SchurScratch<10>) <= sizeof(double) * 60 * 66, "scratch must fit in Q");
+
+// ---- cross-lane pieces ---------------------------------------------------------------------------
+// acc[l % 4] += bcast_l(x) * c[l] for the 16 lanes l of x's DPP row (four accumulators in rotation:
+// each is re-read four instructions after its last write).  Hazard: x and c may have been written
+// by VALU just before (2 wait states) or EXEC by a branch (5): the leading s_nop 4.
+#define SC_F(A, C, L) "v_fmac_f64_dpp %[" A "], %[x], %[" C "] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ void mv16(double x, const double* c, double& a0, double& a1, double& a2, double& a3) {
+  asm("s_nop 4\n\t"
+      SC_F("a0", "c0", 0) SC_F("a1", "c1", 1) SC_F("a2", "c2", 2) SC_F("a3", "c3", 3)
+      SC_F("a0", "c4", 4) SC_F("a1", "c5", 5) SC_F("a2", "c6", 6) SC_F("a3", "c7", 7)
+      SC_F("a0", "c8", 8) SC_F("a1", "c9", 9) SC_F("a2", "c10", 10) SC_F("a3", "c11", 11)
+      SC_F("a0", "c12", 12) SC_F("a1", "c13", 13) SC_F("a2", "c14", 14) SC_F("a3", "c15", 15)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
+      : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
+        [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]),
+        [c11] "v"(c[11]), [c12] "v"(c[12]), [c13] "v"(c[13]), [c14] "v"(c[14]), [c15] "v"(c[15]));
+}
+#undef SC_F
+// s[l] += bcast_l(x) * g for the 16 lanes l of x's DPP row (a rank-1 row update; independent
+// destinations, so no accumulator latency).
+#define SC_U(L) "v_fmac_f64_dpp %[s" #L "], %[x], %[g] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ void upd16(double x, double g, double* s) {
+  asm("s_nop 4\n\t"
+      SC_U(0) SC_U(1) SC_U(2) SC_U(3) SC_U(4) SC_U(5) SC_U(6) SC_U(7)
+      SC_U(8) SC_U(9) SC_U(10) SC_U(11) SC_U(12) SC_U(13) SC_U(14) SC_U(15)
+      : [s0] "+v"(s[0]), [s1] "+v"(s[1]), [s2] "+v"(s[2]), [s3] "+v"(s[3]), [s4] "+v"(s[4]), [s5] "+v"(s[5]),
+        [s6] "+v"(s[6]), [s7] "+v"(s[7]), [s8] "+v"(s[8]), [s9] "+v"(s[9]), [s10] "+v"(s[10]),
+        [s11] "+v"(s[11]), [s12] "+v"(s[12]), [s13] "+v"(s[13]), [s14] "+v"(s[14]), [s15] "+v"(s[15])
+      : [x] "v"(x), [g] "v"(g));
+}
+#undef SC_U
+
+// alpha_jl of M (integer valued, exact in binary64): sum_{i=max(j,l)}^{N-1} (i - j)(i - l)
+__device__ __forceinline__ double alpha_jl(int N, int j, int l) {
+  const int M = j > l ? j : l, K = N - 1, cnt = K - M + 1;
+  const int s1 = (M + K) * cnt / 2;
+  const int s2 = K * (K + 1) * (2 * K + 1) / 6 - (M - 1) * M * (2 * M - 1) / 6;
+  return (double)(s2 - (j + l) * s1 + j * l * cnt);
+}
+
+// ---- factorization (once per rho) ----------------------------------------------------------------
+// Inputs: sc.Rt (R'_k foot blocks, written by the caller's variable lanes), sm.Bw.  Outputs: Q in
+// LDS and, per lane, RI[r][3] (row a of R'^-1 of its foot, variable role), BC[r][6] (column
+// 3 leg + a of B_k, variable role) and BR[12] (row c of B_k, impulse role).
+template <int N, int R, class SM>
+__device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp_params& p, const Adisc& A, double cost_c,
+                             double dtm, double (&RI)[R][3], double (&BC)[R][6], double (&BR)[12]) {
+  constexpr int NI = SchurCfg<N>::NI;
+  auto& sc = F.s;
+  const int t = threadIdx.x, q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
+  const bool av = a < 3;
+  const int ig = gray(q);
+  // R'^-1 per foot (cofactor inverse of the symmetric 3x3): the variable lane's row a
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int k = 4 * r + ig;
+    const int kc = k < N ? k : N - 1;
+    const double* m = sc.Rt[kc][leg];
+    const double m00 = m[0], m01 = m[1], m02 = m[2], m11 = m[3], m12 = m[4], m22 = m[5];
+    const double c00 = m11 * m22 - m12 * m12, c01 = m02 * m12 - m01 * m22, c02 = m01 * m12 - m02 * m11;
+    const double c11 = m00 * m22 - m02 * m02, c12 = m01 * m02 - m00 * m12, c22 = m00 * m11 - m01 * m01;
+    const double inv = 1.0 / ((m00 * c00 + m01 * c01) + m02 * c02);
+    const double i0 = sel3(a, c00, c01, c02) * inv, i1 = sel3(a, c01, c11, c12) * inv,
+                 i2 = sel3(a, c02, c12, c22) * inv;
+    if (k < N && av) {
+      sc.Ri[k][leg][3 * a + 0] = i0;
+      sc.Ri[k][leg][3 * a + 1] = i1;
+      sc.Ri[k][leg][3 * a + 2] = i2;
+    }
+  }
+  wave_sync();
+  // impulse role: lane i = 6 k + c
+  const int i = t < NI ? t : NI - 1;
+  const bool iv = t < NI;
+  const int k = i / 6, c = i % 6;
+  // row c of B6 R'^-1: rows 0-2 of B6 are B_w (3 x 12), rows 3-5 dt/m on the matching component
+  double br[12];
+#pragma unroll
+  for (int l = 0; l < 4; ++l)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const double* ri = sc.Ri[k][l];
+      double s;
+      if (c < 3) {
+        const double* bw = sm.Bw[k][c < 3 ? c : 0] + 3 * l;
+        s = (bw[0] * ri[b] + bw[1] * ri[3 + b]) + bw[2] * ri[6 + b];
+      } else {
+        s = dtm * ri[3 * (c - 3) + b];
+      }
+      br[3 * l + b] = s;
+    }
+  if (iv)
+#pragma unroll
+    for (int j = 0; j < 12; ++j) sc.B6R[i][j] = br[j];
+  // row c of G_k = (B6 R'^-1)_k B6_k'; the Cholesky below reads only its lower triangle, each entry
+  // written by exactly one lane
+#pragma unroll
+  for (int d = 0; d < 6; ++d) {
+    double s;
+    if (d < 3) {
+      const double* bw = sm.Bw[k][d];
+      s = 0.0;
+#pragma unroll
+      for (int j = 0; j < 12; ++j) s += br[j] * bw[j];
+    } else {
+      s = dtm * (((br[d - 3] + br[d]) + br[d + 3]) + br[d + 6]);
+    }
+    if (iv && d <= c) sc.G[k][6 * c + d] = s;
+  }
+  wave_sync();
+  // Cholesky G_k = L L' and Li = L^-1 (every lane of the step, redundantly)
+  double L[6][6], Li[6][6];
+#pragma unroll
+  for (int r2 = 0; r2 < 6; ++r2)
+#pragma unroll
+    for (int c2 = 0; c2 < 6; ++c2) L[r2][c2] = 0.0;
+#pragma unroll
+  for (int cc = 0; cc < 6; ++cc) {
+    double s = sc.G[k][6 * cc + cc];
+#pragma unroll
+    for (int e = 0; e < cc; ++e) s -= L[cc][e] * L[cc][e];
+    const double dg = sqrt(s), dinv = 1.0 / dg;
+    L[cc][cc] = dg;
+#pragma unroll
+    for (int r2 = cc + 1; r2 < 6; ++r2) {
+      double v = sc.G[k][6 * r2 + cc];
+#pragma unroll
+      for (int e = 0; e < cc; ++e) v -= L[r2][e] * L[cc][e];
+      L[r2][cc] = v * dinv;
+    }
+  }
+#pragma unroll
+  for (int cc = 0; cc < 6; ++cc) {  // forward substitution, column cc of L^-1
+#pragma unroll
+    for (int r2 = 0; r2 < 6; ++r2) {
+      if (r2 < cc) {
+        Li[r2][cc] = 0.0;
+        continue;
+      }
+      double v = r2 == cc ? 1.0 : 0.0;
+#pragma unroll
+      for (int e = cc; e < r2; ++e) v -= L[r2][e] * Li[e][cc];
+      Li[r2][cc] = v / L[r2][r2];
+    }
+  }
+  // the lane's column c of L and row c of Li (c is per lane: selects, not register indexing)
+  double Lc[6], lic[6];
+#pragma unroll
+  for (int e = 0; e < 6; ++e) {
+    double v = L[e][0], w = Li[0][e];
+#pragma unroll
+    for (int cc = 1; cc < 6; ++cc) {
+      v = c == cc ? L[e][cc] : v;
+      w = c == cc ? Li[cc][e] : w;
+    }
+    Lc[e] = v;
+    lic[e] = w;
+  }
+  // row c of B = Li (B6 R'^-1)
+  double bl[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) s += lic[e] * sc.B6R[6 * k + e][j];
+    bl[j] = s;
+  }
+  // columns of sqrt(c) Qv^1/2 L_k and sqrt(c) Qp^1/2 Ac6 L_k (Ac6 = A[0:6, 6:12])
+  double vw[12];
+#pragma unroll
+  for (int e = 0; e < 6; ++e) vw[e] = sqrt(cost_c * (2.0 * p.q_weights[6 + e])) * Lc[e];
+#pragma unroll
+  for (int e = 0; e < 6; ++e) {
+    double s = 0.0;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) s += A.at(e, 6 + f) * Lc[f];
+    vw[6 + e] = sqrt(cost_c * (2.0 * p.q_weights[e])) * s;
+  }
+  // sc.B6R is read above by every lane before any lane writes BL / VW (in-order LDS of one wave)
+  if (iv)
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      sc.BL[i][j] = bl[j];
+      sc.VW[i][j] = vw[j];
+    }
+  wave_sync();
+  // S = I + L'CL, row i in absolute column order (pads: identity).  S[i][m] is computed as the
+  // same dot products in the same order by lanes i and m, so S is exactly symmetric.
+  double S[64];
+#pragma unroll
+  for (int m = 0; m < 64; ++m) {
+    if (m < NI) {
+      const int l = m / 6;
+      const double* o = sc.VW[m];
+      double dv = 0.0, dw = 0.0;
+#pragma unroll
+      for (int e = 0; e < 6; ++e) {
+        dv += vw[e] * o[e];
+        dw += vw[6 + e] * o[6 + e];
+      }
+      const int mx = k > l ? k : l;
+      const double s = (double)(N - mx) * dv + alpha_jl(N, k, l) * dw;
+      S[m] = iv ? (t == m ? 1.0 + s : s) : (t == m ? 1.0 : 0.0);
+    } else {
+      S[m] = t == m ? 1.0 : 0.0;
+    }
+  }
+  // in-place Gauss-Jordan inverse of S (SPD: no pivoting).  With pivots 0..p-1 done, the current
+  // matrix X has X[p][j] = X[j][p] for j >= p and X[p][j] = -X[j][p] for j < p, so row p is lane
+  // j's own column p with a sign: each pivot makes four 16-lane row copies of it with the
+  // row-swap permutes and every lane applies X[t][j] += X[p][j] g_t with row_newbcast FMAs.
+  const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
+  sfor<0, NI>([&](auto P) __attribute__((always_inline)) {
+    constexpr int pv = decltype(P)::value;
+    const double col = S[pv];
+    const double a0 = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(col), pv),
+                                       __builtin_amdgcn_readlane(__double2loint(col), pv));
+    const double pinv = recip(a0);
+    const double rj = t < pv ? -col : col;
+    const double g = t == pv ? pinv - 1.0 : -(col * pinv);
+    const double newc = t == pv ? pinv : -(col * pinv);
+    // row p in every DPP row: copy s' (source row s') of lane (q, l) is rj of lane (s', l), the
+    // lane's own value when q == s', else its row-swap partner q ^ s'
+    const double r16 = xor16(rj), r32 = xor32(rj), r48 = xor32(r16);
+    // copy s' = the value of row q ^ (q ^ s'): bit 0 of q ^ s' picks the row-pair partner, bit 1
+    // the other pair (two levels of v_cndmask on the lane's row bits, no branches)
+    const double e0 = qb0 ? r16 : rj, e1 = qb0 ? rj : r16;    // rows {q, q^1} as seen from bit 0
+    const double f0 = qb0 ? r48 : r32, f1 = qb0 ? r32 : r48;  // rows {q^2, q^3}
+    const double x0 = qb1 ? f0 : e0, x1 = qb1 ? f1 : e1, x2 = qb1 ? e0 : f0, x3 = qb1 ? e1 : f1;
+    upd16(x0, g, S);
+    upd16(x1, g, S + 16);
+    upd16(x2, g, S + 32);
+    upd16(x3, g, S + 48);
+    S[pv] = newc;
+  });
+  // the lane's register factors, read back from the scratch (before Q overwrites it)
+#pragma unroll
+  for (int j = 0; j < 12; ++j) BR[j] = iv ? sc.BL[i][j] : 0.0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int kk = 4 * r + ig;
+    const int kc = kk < N ? kk : N - 1;
+    const int col = 3 * leg + (av ? a : 2);
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) BC[r][cc] = sc.BL[6 * kc + cc][col];
+    const double* ri = sc.Ri[kc][leg] + 3 * (av ? a : 2);
+    RI[r][0] = ri[0];
+    RI[r][1] = ri[1];
+    RI[r][2] = ri[2];
+  }
+  wave_sync();
+  // Q = I - S^-1 (pads and columns >= NI: 0)
+  if (iv) {
+#pragma unroll
+    for (int m = 0; m < 64; m += 2) {
+      const double q0 = m < NI ? (t == m ? 1.0 : 0.0) - S[m] : 0.0;
+      const double q1 = m + 1 < NI ? (t == m + 1 ? 1.0 : 0.0) - S[m + 1] : 0.0;
+      *reinterpret_cast<double2*>(&F.Q[i][m]) = make_double2(q0, q1);
+    }
+  }
+  wave_sync();
+}
+
+// ---- KKT solve (every ADMM iteration) ------------------------------------------------------------
+// W[r]: w = D^-1 rhs in the variable layout; returns U[r] = (c B6'M B6 + R')^-1 w.
+template <int N, int R>
+__device__ __forceinline__ void schur_solve(SchurLds<N>& F, const double (&W)[R], const double (&RI)[R][3],
+                                            const double (&BC)[R][6], const double (&BR)[12], const bool (&vvr)[R],
+                                            double (&U)[R]) {
+  constexpr int NI = SchurCfg<N>::NI;
+  const int t = threadIdx.x, q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
+  const bool av = a < 3;
+  const int ig = gray(q);
+  const int idx = 3 * leg + (av ? a : 2);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (vvr[r]) F.wv[12 * (4 * r + ig) + idx] = W[r];
+  wave_sync();
+  // impulse role: z = B w of the lane's step, then q = Q z
+  const int i = t < NI ? t : NI - 1;
+  const int k = i / 6;
+  double z = 0.0;
+  {
+    const double2* w2 = reinterpret_cast<const double2*>(&F.wv[12 * k]);
+    double za = 0.0, zb = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const double2 v = w2[j];
+      za = fma(BR[2 * j], v.x, za);
+      zb = fma(BR[2 * j + 1], v.y, zb);
+    }
+    z = t < NI ? za + zb : 0.0;
+  }
+  const double z1 = xor16(z), z2 = xor32(z), z3 = xor32(z1);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  {
+    const double* qr = F.Q[i];
+    double c[16];
+    auto load = [&](int s) __attribute__((always_inline)) {
+      const double2* p2 = reinterpret_cast<const double2*>(qr + 16 * (q ^ s));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double2 v = p2[e];
+        c[2 * e] = v.x;
+        c[2 * e + 1] = v.y;
+      }
+    };
+    load(0);
+    mv16(z, c, a0, a1, a2, a3);
+    load(1);
+    mv16(z1, c, a0, a1, a2, a3);
+    load(2);
+    mv16(z2, c, a0, a1, a2, a3);
+    load(3);
+    mv16(z3, c, a0, a1, a2, a3);
+  }
+  const double qi = (a0 + a1) + (a2 + a3);
+  if (t < NI) F.qv[t] = qi;
+  wave_sync();
+  // variable role: u = R'^-1 w - B' q
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int kk = 4 * r + ig;
+    const int kc = kk < N ? kk : N - 1;
+    const double* wf = &F.wv[12 * kc + 3 * leg];
+    const double r1 = (RI[r][0] * wf[0] + RI[r][1] * wf[1]) + RI[r][2] * wf[2];
+    const double2* q2 = reinterpret_cast<const double2*>(&F.qv[6 * kc]);
+    const double2 qa = q2[0], qb = q2[1], qc = q2[2];
+    const double y = ((((BC[r][0] * qa.x + BC[r][1] * qa.y) + BC[r][2] * qb.x) + BC[r][3] * qb.y) + BC[r][4] * qc.x) +
+                     BC[r][5] * qc.y;
+    U[r] = r1 - y;
+  }
+}
+
+}  // namespace wv
+}  // namespace mpcqp

@@ -32,7 +32,7 @@
 // lane) and row 4 (fz bounds, replicated), so every per-foot ADMM operation (A~x, A~'y, the
 // projection) is a quad-perm DPP.  No barrier exists anywhere: the workgroup is the wave.
 // Arithmetic is binary64 throughout.
-#include "mpcqp_wave_common.h"
+#include "mpcqp_schur.h"
 
 namespace mpcqp {
 namespace wv {
@@ -337,7 +337,9 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   } while (0)
 #endif
 
-template <int N>
+// KS: the KKT solve.  0 = Riccati recursion (chains over the horizon, factors on MFMA; every N),
+// 1 = impulse-space Schur form (mpcqp_schur.h; N <= 10, nonnegative state weights).
+template <int N, int KS>
 __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ recs, int batch,
                                                      mpcqp_result* __restrict__ results,
                                                      double* __restrict__ solution, double* __restrict__ trace,
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   using C = Cfg<N>;
   using WL = WarmLayout<N>;
   constexpr int n = C::n, m = C::m, R = C::R;
-  __shared__ WSmem<N> sm;
+  __shared__ WSmem<N, KS> sm;
   const int inst = blockIdx.x;
   if (inst >= batch) return;
   const int t = threadIdx.x;
@@ -385,7 +387,13 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   wave_sync();
   WV_MARK(1);
   const double* rec = HS.rec;
-  const double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS], mu = rec[MPCQP_REC_MU];
+  // Record values used after the setup image is recycled (the LDS union is rewritten by the
+  // factorization) are pinned into registers: keep() hides their origin, so the compiler cannot
+  // rematerialize them by reloading the (by then overwritten) LDS words.
+  double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS], mu = rec[MPCQP_REC_MU];
+  keep(dt);
+  keep(mass);
+  keep(mu);
   Adisc A;
   {
     const double yaw = rec[MPCQP_REC_EULER + 2];
@@ -394,12 +402,13 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     A.dt = dt;
   }
   const double dtm = (1.0 / mass) * dt;
-  // what the solve needs from the record after the setup image is recycled
-  double Rot[9];
-#pragma unroll
-  for (int e = 0; e < 9; ++e) Rot[e] = rec[MPCQP_REC_ROT + e];
-  const double cont = rec[MPCQP_REC_CONTACTS + leg] != 0.0 ? 1.0 : 0.0;
-  const double fzmin = rec[MPCQP_REC_FZMIN], fzmax = rec[MPCQP_REC_FZMAX];
+  // what the solve needs from the record after the setup image is recycled (root_rot_mat is read
+  // again from HBM by the epilogue)
+  double cont = rec[MPCQP_REC_CONTACTS + leg] != 0.0 ? 1.0 : 0.0;
+  double fzmin = rec[MPCQP_REC_FZMIN], fzmax = rec[MPCQP_REC_FZMAX];
+  keep(cont);
+  keep(fzmin);
+  keep(fzmax);
 
   // ---- 1. B_d(k) rows 6-8 (calculate_B_mat_c, Utils.cpp:35-41), gradient adjoint --------------------
   {
@@ -447,9 +456,11 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   // ---- 4. lane registers: variables (D, q~) and rows (E, A~, bounds, rho) — set_rho_vec -----------
   // update_P keeps the adapted rho (settings->rho); setup and re-init start from the settings'
   const double rho0 = mode == 1 ? ws[WL::RHO] : dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
-  double X[R], Qv[R], Dv[R], DI[R], PX[R], PXO[R], DX[R], RHS[R];
-  double Z[R], Y[R], DY[R], Ev[R], AK0[R], AK1[R];
-  double Z4[R], Y4[R], DY4[R], E4[R], L4[R], U4[R], AK4[R], RHO4[R];
+  // Dv, Ev, E4 are setup-only arrays: the loop reads D and E from the image again when it needs
+  // them (factorizations, termination checks, the epilogue) instead of holding them in registers
+  double X[R], Qv[R], Dv[R], DI[R], PX[R], RHS[R];
+  double Z[R], Y[R], Ev[R], AK0[R], AK1[R];
+  double Z4[R], Y4[R], E4[R], L4[R], U4[R], AK4[R], RHO4[R];
   bool kvr[R], vvr[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -476,8 +487,8 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     u4 = dmin(dmax(u4, -OSQP_INF), OSQP_INF);
     L4[r] = E4[r] * l4;
     U4[r] = E4[r] * u4;
-    X[r] = 0.0; PX[r] = 0.0; PXO[r] = 0.0; DX[r] = 0.0;
-    Z[r] = 0.0; Y[r] = 0.0; DY[r] = 0.0; Z4[r] = 0.0; Y4[r] = 0.0; DY4[r] = 0.0;
+    X[r] = 0.0; PX[r] = 0.0;
+    Z[r] = 0.0; Y[r] = 0.0; Z4[r] = 0.0; Y4[r] = 0.0;
     RHS[r] = vv ? sigma * 0.0 - Qv[r] : 0.0;  // cold start: compute_rhs with x = z = y = 0
     if (mode == 1) {  // warm start: the previous scaled iterates as they are
       X[r] = vv ? ws[WL::X + ci] : 0.0;
@@ -559,16 +570,31 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       RHS[r] = vvr[r] ? (sigma * X[r] - Qv[r]) + at : 0.0;
     }
   }
+  // D and E of the lane's variable / rows, reloaded from the image (volatile: never hoisted into
+  // loop-carried registers)
+  const volatile double* imv = im;
+  auto dv_of = [&](int r) __attribute__((always_inline)) {
+    return vvr[r] ? imv[SI::D + ND * (4 * r + ig) + idx] : 1.0;
+  };
+  auto ev_of = [&](int r) __attribute__((always_inline)) {
+    return kvr[r] ? imv[SI::E + CD * (4 * r + ig) + 5 * leg + a] : 1.0;
+  };
+  auto e4_of = [&](int r) __attribute__((always_inline)) {
+    return kvr[r] ? imv[SI::E + CD * (4 * r + ig) + 5 * leg + 4] : 1.0;
+  };
   // rows 0-3: l = 0 / u = +inf (rows 0, 2) or l = -inf / u = 0 (rows 1, 3): always inequalities
-  auto lo03 = [&](int r) __attribute__((always_inline)) { return (a & 1) ? Ev[r] * -OSQP_INF : Ev[r] * 0.0; };
+  auto lo03 = [&](double ev) __attribute__((always_inline)) { return (a & 1) ? ev * -OSQP_INF : ev * 0.0; };
   // the projection onto those bounds needs no E: [0, +inf) for rows 0, 2, (-inf, 0] for rows 1, 3
   // (equal to clamping at E * -+OSQP_INF for every operand below 1e30 E in magnitude)
   const double LO03 = (a & 1) ? -INFINITY : 0.0, HI03 = (a & 1) ? 0.0 : INFINITY;
-  auto hi03 = [&](int r) __attribute__((always_inline)) { return (a & 1) ? Ev[r] * 0.0 : Ev[r] * OSQP_INF; };
+  auto hi03 = [&](double ev) __attribute__((always_inline)) { return (a & 1) ? ev * 0.0 : ev * OSQP_INF; };
   wave_sync();  // every LDS read of the setup image precedes its reuse by the factorization
 
   // ---- 5. ADMM (osqp_solve) ------------------------------------------------------------------------
   auto& F = sm.u.f;
+  // KS = 1: the lane's rows / columns of the Schur-form factors (mpcqp_schur.h), set per rho
+  double SRI[KS == 1 ? R : 1][3], SBC[KS == 1 ? R : 1][6], SBR[12];
+  (void)SRI; (void)SBC; (void)SBR;
   double rho = rho0, rinv = 1. / rho0, pri_res = 0.0, dua_res = 0.0;
   int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
   bool need_factor = true;
@@ -583,7 +609,8 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                      k03 = dpp<QP_B3>(AK0[r]);
         const double k10 = dpp<QP_B0>(AK1[r]), k11 = dpp<QP_B1>(AK1[r]), k12 = dpp<QP_B2>(AK1[r]),
                      k13 = dpp<QP_B3>(AK1[r]);
-        const double d0 = dpp<QP_B0>(Dv[r]), d1 = dpp<QP_B1>(Dv[r]), d2 = dpp<QP_B2>(Dv[r]);
+        const double dvr = dv_of(r);
+        const double d0 = dpp<QP_B0>(dvr), d1 = dpp<QP_B1>(dvr), d2 = dpp<QP_B2>(dvr);
         const double ak4 = AK4[r], r4 = RHO4[r];
         // rows of the foot: r0 [k00,0,k10] r1 [k01,0,k11] r2 [0,k02,k12] r3 [0,k03,k13] r4 [0,0,ak4]
         auto coef = [&](int row, int col) __attribute__((always_inline)) {
@@ -603,11 +630,15 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
           const double db = b == 0 ? d0 : (b == 1 ? d1 : d2);
           const double rt = (av && a == b ? cost_c * (2.0 * p.r_weights[idx]) : 0.0) +
                             ((1.0 / da) * ((av && a == b ? sigma : 0.0) + s)) * (1.0 / db);
-          if (kvr[r] && av && b >= a) F.Rt[k][leg][sym6(a, b)] = rt;
+          if (kvr[r] && av && b >= a) {
+            if constexpr (KS == 0) F.Rt[k][leg][sym6(a, b)] = rt;
+            else F.s.Rt[k][leg][sym6(a, b)] = rt;
+          }
         }
       }
       wave_sync();
-      factorize_mfma<N>(sm, p, A, cost_c, dtm);
+      if constexpr (KS == 0) factorize_mfma<N>(sm, p, A, cost_c, dtm);
+      else schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI, SBC, SBR);
       wave_sync();
       need_factor = false;
       WV_MARK(12);
@@ -617,7 +648,12 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     double U[R];
     const bool tm_it = iter == 60;
     if (tm_it) WV_MARK(40);
-    {
+    if constexpr (KS == 1) {
+      double W[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) W[r] = DI[r] * RHS[r];
+      schur_solve<N, R>(F, W, SRI, SBC, SBR, vvr, U);
+    } else {
       // LDS operands are loaded one phase ahead of their use; sched_barrier keeps the scheduler from
       // sinking a prefetch back down to its consumer (counted lgkmcnt waits then cover only it).
       double W[R], AKw[R], SMv[R], G[R], Hh[R], XS[R], tt[R];
@@ -652,7 +688,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       // The chains load Acl one ROUND at a time: DPP row q takes the matrix of step 4 rr + gray(q) of
       // round rr, the step that row computes (every chain step runs in the row of its step), so one
       // 12-double load per lane serves four chain steps.
-      constexpr int NA = WSmem<N>::NA;
+      constexpr int NA = WSmem<N, KS>::NA;
       auto aslot = [&](int rr) __attribute__((always_inline)) { return min(max(4 * rr + ig - 1, 0), NA - 1); };
       if constexpr (N >= 3) ldcol(cn, &F.Acl[aslot((N - 2) >> 2)][idx]);
       __builtin_amdgcn_sched_barrier(0);
@@ -797,6 +833,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     const bool need_info = is_check || is_adapt || last;
 
     // ---- update_x / update_z / update_y, and P~x by the KKT identity P~x~ = rhs - sigma x~ - A~'rho A~x~
+    // this iteration's deltas, for the infeasibility tests of a need_info iteration only
+    double DX[R], DY[R], DY4[R], PXO[R];
+    auto update = [&](auto INFO) __attribute__((always_inline)) {
+      constexpr bool info = decltype(INFO)::value;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const double xt = DI[r] * U[r];
@@ -809,7 +849,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         const double dyv = rho * (zr - zn);
         Z[r] = zn;
         Y[r] = Y[r] + dyv;
-        DY[r] = dyv;
+        if constexpr (info) DY[r] = dyv;
       }
       {
         const double r4 = RHO4[r];
@@ -818,22 +858,25 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         const double dyv = r4 * (zr - zn);
         Z4[r] = zn;
         Y4[r] = Y4[r] + dyv;
-        DY4[r] = dyv;
+        if constexpr (info) DY4[r] = dyv;
       }
       const double kd = quad_at(rho * zt, RHO4[r] * zt4, AK0[r], AK1[r], AK4[r], a);
       // every lane updates (values of padding lanes / steps past N are never read unmasked)
       const double xo = X[r];
       const double xn = alpha * xt + (1.0 - alpha) * xo;
-      DX[r] = xn - xo;
+      if constexpr (info) DX[r] = xn - xo;
       X[r] = xn;
       const double pxt = (RHS[r] - sigma * xt) - kd;
-      PXO[r] = PX[r];
+      if constexpr (info) PXO[r] = PX[r];
       PX[r] = alpha * pxt + (1.0 - alpha) * PX[r];
       // next right-hand side sigma x - q~ + A~'(rho z - y), here so that it interleaves with the other
       // rounds' updates (recomputed below when adapt_rho changes rho)
       const double at = quad_at(rho * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
       RHS[r] = (sigma * X[r] - Qv[r]) + at;
     }
+    };
+    if (need_info) update(IC<1>{});
+    else update(IC<0>{});
 
     if (tm_it) WV_MARK(46);
     if (need_info) {
@@ -847,7 +890,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         const double ax = AK0[r] * xp + AK1[r] * xz, ax4 = AK4[r] * xz;
         const double aty = quad_at(Y[r], Y4[r], AK0[r], AK1[r], AK4[r], a);
         if (kvr[r]) {
-          const double ei = 1.0 / Ev[r], ei4 = 1.0 / E4[r];
+          const double ei = 1.0 / ev_of(r), ei4 = 1.0 / e4_of(r);
           const double pr = ax + (-1.0) * Z[r], pr4 = ax4 + (-1.0) * Z4[r];
           mx[0] = dmax(mx[0], dmax(dabs(ei * pr), dabs(ei4 * pr4)));
           mx[1] = dmax(mx[1], dmax(dabs(pr), dabs(pr4)));
@@ -894,12 +937,13 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
               }
               return d;
             };
-            const double lo = lo03(r), hi = hi03(r);
+            const double evr = ev_of(r), e4r = e4_of(r);
+            const double lo = lo03(evr), hi = hi03(evr);
             const double d = proj(DY[r], lo, hi), d4 = proj(DY4[r], L4[r], U4[r]);
             dyp[r] = d;
             dyp4[r] = d4;
             if (kvr[r]) {
-              nd = dmax(nd, dmax(dabs(Ev[r] * d), dabs(E4[r] * d4)));
+              nd = dmax(nd, dmax(dabs(evr * d), dabs(e4r * d4)));
               lh += hi * dmax(d, 0.0) + lo * dmin(d, 0.0);
               if (a == 0) lh += U4[r] * dmax(d4, 0.0) + L4[r] * dmin(d4, 0.0);
             }
@@ -927,7 +971,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 #pragma unroll
           for (int r = 0; r < R; ++r)
             if (vvr[r]) {
-              nx = dmax(nx, dabs(Dv[r] * DX[r]));
+              nx = dmax(nx, dabs(dv_of(r) * DX[r]));
               qd += Qv[r] * DX[r];
             }
           const double ndx = wave_max(nx);
@@ -944,9 +988,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                   const double dp = dpp<QP_PRIM>(DX[r]), dz = dpp<QP_B2>(DX[r]);
-                  const double v = (1.0 / Ev[r]) * (AK0[r] * dp + AK1[r] * dz);
-                  const double v4 = (1.0 / E4[r]) * (AK4[r] * dz);
-                  const double lo = lo03(r), hi = hi03(r);
+                  const double evr = ev_of(r);
+                  const double v = (1.0 / evr) * (AK0[r] * dp + AK1[r] * dz);
+                  const double v4 = (1.0 / e4_of(r)) * (AK4[r] * dz);
+                  const double lo = lo03(evr), hi = hi03(evr);
                   if (kvr[r]) {
                     if ((hi < OSQP_INF * MIN_SCALING && v > eps_dinf * ndx) ||
                         (lo > -OSQP_INF * MIN_SCALING && v < -eps_dinf * ndx))
@@ -1029,19 +1074,19 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       const int k = 4 * r + ig;
       if (vvr[r]) {
         const int ci = ND * k + idx;
-        ws[WL::D + ci] = Dv[r];
+        ws[WL::D + ci] = dv_of(r);
         ws[WL::QT + ci] = Qv[r];
         ws[WL::X + ci] = X[r];
       }
       if (kvr[r]) {
         const int ri = CD * k + 5 * leg + a, r4 = CD * k + 5 * leg + 4;
-        ws[WL::E + ri] = Ev[r];
+        ws[WL::E + ri] = ev_of(r);
         ws[WL::AK + ri] = AK0[r];
         ws[WL::AK + m + ri] = AK1[r];
         ws[WL::Z + ri] = Z[r];
         ws[WL::Y + ri] = Y[r];
         if (a == 0) {
-          ws[WL::E + r4] = E4[r];
+          ws[WL::E + r4] = e4_of(r);
           ws[WL::AK + r4] = 0.0;
           ws[WL::AK + m + r4] = AK4[r];
           ws[WL::Z + r4] = Z4[r];
@@ -1063,12 +1108,16 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   double xs0 = 0.0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const double xs = has_sol ? Dv[r] * X[r] : NAN;
+    const double xs = has_sol ? dv_of(r) * X[r] : NAN;
     if (r == 0) xs0 = xs;
     if (solution && vvr[r]) solution[(size_t)inst * n + ND * (4 * r + ig) + idx] = xs;
   }
   // u0 = step 0 = round 0, DPP row 0 (lanes 0..15); f_i = R^T u0[3i:3i+3], NaN legs skipped
   mpcqp_result* res = results + inst;
+  const volatile double* rotv = recs + (size_t)inst * C::REC + MPCQP_REC_ROT;
+  double Rot[9];
+#pragma unroll
+  for (int e = 0; e < 9; ++e) Rot[e] = rotv[e];
   const double u00 = dpp<QP_B0>(xs0), u01 = dpp<QP_B1>(xs0), u02 = dpp<QP_B2>(xs0);
   const double nrm = sqrt(u00 * u00 + u01 * u01 + u02 * u02);
   const bool nanleg = isnan(nrm);
@@ -1116,13 +1165,31 @@ __global__ void wave_selftest_kernel(double* out) {
 
 }  // namespace wv
 
+// The Schur-form KKT solve serves N <= 10 with nonnegative state weights (it factors Q with square
+// roots); the Riccati recursion everything else.
+static bool schur_ok(const mpcqp_params& p) {
+  if (p.horizon > 10) return false;
+  for (int i = 0; i < MPCQP_STATE_DIM; ++i)
+    if (!(p.q_weights[i] >= 0.0)) return false;
+#ifdef MPCQP_WAVE_RICCATI_ONLY
+  return false;
+#endif
+  return true;
+}
 template <int N>
 static hipError_t launch_wave(const LaunchArgs& a) {
   hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
                      a.recs, a.batch, a.wstate, a.work, a.p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((wv::wave_kernel<N>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs, a.batch,
+  if constexpr (N <= 10) {
+    if (schur_ok(a.p)) {
+      hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs,
+                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((wv::wave_kernel<N, 0>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs, a.batch,
                      a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p);
   return hipGetLastError();
 }
@@ -1134,11 +1201,14 @@ static hipError_t launch_scale(const LaunchArgs& a) {
 }
 template <int N>
 static hipError_t occupancy_wave(int* blocks) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wv::wave_kernel<N>, wv::NT, 0);
+  if constexpr (N <= 10) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wv::wave_kernel<N, 1>, wv::NT, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wv::wave_kernel<N, 0>, wv::NT, 0);
 }
 
+#ifndef MPCQP_WAVE_FOR_EACH_N
 #define MPCQP_WAVE_FOR_EACH_N(X) \
   X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20)
+#endif
 
 hipError_t launch_wave_any(const LaunchArgs& a) {
   switch (a.p.horizon) {

@@ -3,6 +3,8 @@
 // discrete dynamics, the MFMA Riccati factorization, and the scale_kernel image layout.
 // Not installed.
 #pragma once
+#include <type_traits>
+
 #include "mpcqp_device.h"
 
 
@@ -42,6 +44,8 @@ constexpr int MS = 146;
 __host__ __device__ constexpr int mo(int r) { return 12 * r + (r >= 4 ? 2 : 0); }
 
 template <int N>
+struct SchurLds;
+template <int N, int KS>
 struct WSmem {
   using C = Cfg<N>;
   static constexpr int NK = N > 1 ? N - 1 : 1;  // K_k stored for k = 1..N-1
@@ -61,7 +65,9 @@ struct WSmem {
       alignas(16) double K[NK][MS];
       alignas(16) double Acl[NA][MS];
       double Rt[N][4][6];             // R'_k foot blocks, upper triangle (00 01 02 11 12 22)
-    } f;
+    };
+    // KS = 0: the Riccati factors; KS = 1: the impulse-space Schur form (mpcqp_schur.h)
+    typename std::conditional<KS == 0, Fs, SchurLds<N>>::type f;
   } u;
 };
 
@@ -318,18 +324,6 @@ struct Adisc {
   }
 };
 
-// (M B_k)_{rc} = sum_{s=6..11} M[r][s] B_k[s][c]
-template <int N>
-__device__ __forceinline__ double mb(const WSmem<N>& sm, const double* M, int k, int r, int c, double dtm) {
-  const double* mr = M + 12 * r;
-  return ((mr[6] * sm.Bw[k][0][c] + mr[7] * sm.Bw[k][1][c]) + mr[8] * sm.Bw[k][2][c]) + mr[9 + c % 3] * dtm;
-}
-// (B_k' M)_{ij} = sum_{s=6..11} B_k[s][i] M[s][j]
-template <int N>
-__device__ __forceinline__ double btm(const WSmem<N>& sm, const double* M, int k, int i, int j, double dtm) {
-  return ((sm.Bw[k][0][i] * M[72 + j] + sm.Bw[k][1][i] * M[84 + j]) + sm.Bw[k][2][i] * M[96 + j]) +
-         dtm * M[12 * (9 + i % 3) + j];
-}
 
 // I_w^-1, I_w = R I_b R' (calculate_B_mat_c, ConvexMpc.cpp:132-138; Eigen's cofactor inverse)
 __device__ __forceinline__ void iw_inverse(const double* rec, double (&Iwinv)[9]) {

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""In-kernel phase timing of the default solve (wave_kernel): run a library built with
+-DMPCQP_PHASE_TIMING (`make -C go1-qp-mpc-controller_amd variant OUT=../abtest/timing.so
+DEFS=-DMPCQP_PHASE_TIMING`, selected with MPCQP_LIB) and report median shader-clock cycles per
+robot: setup (marks 0 -> 4), each factorization (10 -> 12), the mean ADMM iteration (loop time
+minus factorizations over the iteration count) and, inside iteration 60, the KKT solve (40 -> 45),
+the ADMM update (45 -> 46) and the rest of the iteration (46 -> 47)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "go1-qp-mpc-controller_amd"))
+import mpcqp  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--traced", type=int, default=512)
+    ap.add_argument("--horizon", type=int, default=10)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    st = mpcqp.synthetic_go1(a.batch, seed=1000, gait="trot")
+    recs = mpcqp.assemble_compute_grf(st, a.horizon)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(a.horizon)) as s:
+        d_rec = torch.from_numpy(recs).cuda()
+        d_res = torch.zeros((a.batch, mpcqp._lib.RESULT_DOUBLES), dtype=torch.float64, device="cuda")
+        tr = torch.full((a.traced, 64, 4), float("nan"), dtype=torch.float64, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        for _ in range(2):
+            tr.fill_(float("nan"))
+            s.solve_device_trace(d_rec.data_ptr(), a.batch, d_res.data_ptr(), 0, tr.data_ptr(), a.traced, stream)
+        torch.cuda.synchronize()
+        marks = tr.cpu().numpy().reshape(a.traced, 64, 4)
+        res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
+    ph = {k: [] for k in ("setup", "factor", "iter_cycles", "it_kkt", "it_update", "it_rest", "total", "shader_ghz")}
+    for b in range(a.traced):
+        mk = marks[b]
+        mk = mk[~np.isnan(mk[:, 0])]
+        ids, cyc = mk[:, 0].astype(int), mk[:, 1]
+        at = {}
+        for i, c in zip(ids, cyc):
+            at.setdefault(i, []).append(c)
+        ph["shader_ghz"].append((cyc[-1] - cyc[0]) / max(mk[-1, 2] - mk[0, 2], 1) * 0.1)
+        ph["setup"].append(at[4][0] - at[0][0])
+        fac = [at[12][k] - at[10][k] for k in range(min(len(at[10]), len(at.get(12, []))))]
+        ph["factor"] += fac
+        ph["total"].append(at[20][0] - at[0][0])
+        ph["iter_cycles"].append((at[20][0] - at[4][0] - sum(fac)) / max(int(res["iters"][b]), 1))
+        if 40 in at and 45 in at:
+            ph["it_kkt"].append(at[45][0] - at[40][0])
+            ph["it_update"].append(at[46][0] - at[45][0])
+            ph["it_rest"].append(at[47][0] - at[46][0])
+    out = {k: float(np.median(v)) for k, v in ph.items() if v}
+    out["mean_iters"] = float(res["iters"][: a.traced].mean())
+    out["factorizations_per_robot"] = len(ph["factor"]) / a.traced
+    print(json.dumps(out, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
