@@ -34,9 +34,12 @@ template <int N>
 struct SchurCfg {
   static_assert(N >= 1 && N <= 10, "one lane per impulse unknown: 6N <= 64");
   static constexpr int NI = 6 * N;  // impulse unknowns
-  // LDS row stride of Q (doubles): rows 528 B apart put lanes i .. i+7 of a ds_read_b128 on eight
-  // distinct 16-B bank groups (a 512-B stride would put all of them on one)
-  static constexpr int QS = 66;
+  // LDS row stride of Q (doubles).  A row is read as 64 columns, but 62 doubles apart the rows of
+  // lanes i .. i+7 of a ds_read_b128 sit on eight distinct 16-B bank groups (a 512-B stride would
+  // put all of them on one), and the two columns a row reads past its end (62, 63: the next row's
+  // first two, or a zero tail) only ever multiply pad unknowns, whose z is 0.
+  static constexpr int QS = 62;
+  static constexpr int BS = 14;  // row stride of B in LDS: 112 B, conflict-free b128 rows
 };
 
 // Factorization scratch: lives in the rows of Q (which every factorization rewrites at its end).
@@ -47,21 +50,23 @@ struct SchurScratch {
   alignas(16) double Ri[N][4][9];   // R'^-1 foot blocks, row-major
   alignas(16) double B6R[NI][12];   // rows of B6 R'^-1 (step k = i / 6)
   alignas(16) double G[N][36];      // G_k = B_k R'_k^-1 B_k' (row c written by lane 6k + c)
-  alignas(16) double BL[NI][12];    // rows of B = Li B6 R'^-1
   alignas(16) double VW[NI][12];    // columns of sqrt(c) Qv^1/2 L_k and sqrt(c) Qp^1/2 Ac6 L_k
 };
 
 template <int N>
 struct SchurLds {
-  static constexpr int NI = SchurCfg<N>::NI, QS = SchurCfg<N>::QS;
+  static constexpr int NI = SchurCfg<N>::NI, QS = SchurCfg<N>::QS, BS = SchurCfg<N>::BS;
   union {
-    alignas(16) double Q[NI][QS];  // I - S^-1, row i in absolute column order; columns NI..63 zero
+    // I - S^-1: row i at Q + QS i in absolute column order, columns NI .. QS-1 zero, plus a zero
+    // tail for the last row's columns 62, 63
+    alignas(16) double Q[NI * QS + 2];
     SchurScratch<N> s;
   };
+  alignas(16) double Bm[NI][BS];      // B = Li B6 R'^-1: row i = 6 k + c (12 used)
   alignas(16) double wv[12 * N + 4];  // w = D^-1 rhs by variable index 12 k + 3 leg + a
   alignas(16) double qv[64];          // q = Q z by impulse index
 };
-static_assert(sizeof(SchurScratch<10>) <= sizeof(double) * 60 * 66, "scratch must fit in Q");
+static_assert(sizeof(SchurScratch<10>) <= sizeof(double) * (60 * 62 + 2), "scratch must fit in Q");
 
 // ---- cross-lane pieces ---------------------------------------------------------------------------
 // acc[l % 4] += bcast_l(x) * c[l] for the 16 lanes l of x's DPP row (four accumulators in rotation:
@@ -94,6 +99,23 @@ __device__ __forceinline__ void upd16(double x, double g, double* s) {
 }
 #undef SC_U
 
+// Row broadcasts: c_s = the value DPP row s holds, in every DPP row (lane l of each row gets lane
+// l of row s).  permlane16_swap(v, v) gives [r0 r0 r2 r2] / [r1 r1 r3 r3] (rows 0..3), and a
+// permlane32_swap of each of those with itself gives [r0 x4] / [r2 x4] and [r1 x4] / [r3 x4].
+__device__ __forceinline__ void rowbcast4(double v, double& c0, double& c1, double& c2, double& c3) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const auto la = __builtin_amdgcn_permlane32_swap(l16[0], l16[0], false, false);
+  const auto ha = __builtin_amdgcn_permlane32_swap(h16[0], h16[0], false, false);
+  const auto lb = __builtin_amdgcn_permlane32_swap(l16[1], l16[1], false, false);
+  const auto hb = __builtin_amdgcn_permlane32_swap(h16[1], h16[1], false, false);
+  c0 = __hiloint2double((int)ha[0], (int)la[0]);
+  c2 = __hiloint2double((int)ha[1], (int)la[1]);
+  c1 = __hiloint2double((int)hb[0], (int)lb[0]);
+  c3 = __hiloint2double((int)hb[1], (int)lb[1]);
+}
+
 // alpha_jl of M (integer valued, exact in binary64): sum_{i=max(j,l)}^{N-1} (i - j)(i - l)
 __device__ __forceinline__ double alpha_jl(int N, int j, int l) {
   const int M = j > l ? j : l, K = N - 1, cnt = K - M + 1;
@@ -103,12 +125,12 @@ __device__ __forceinline__ double alpha_jl(int N, int j, int l) {
 }
 
 // ---- factorization (once per rho) ----------------------------------------------------------------
-// Inputs: sc.Rt (R'_k foot blocks, written by the caller's variable lanes), sm.Bw.  Outputs: Q in
-// LDS and, per lane, RI[r][3] (row a of R'^-1 of its foot, variable role), BC[r][6] (column
-// 3 leg + a of B_k, variable role) and BR[12] (row c of B_k, impulse role).
-template <int N, int R, class SM>
+// Inputs: sc.Rt (R'_k foot blocks, written by the caller's variable lanes), sm.Bw.  Outputs: Q and
+// B in LDS and, per lane, RI[r][3] (row a of R'^-1 of its foot, variable role).
+template <int N, int R, class SM, class Mark>
 __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp_params& p, const Adisc& A, double cost_c,
-                             double dtm, double (&RI)[R][3], double (&BC)[R][6], double (&BR)[12]) {
+                             double dtm, double (&RI)[R][3], Mark&& mark) {
+  constexpr int QS = SchurCfg<N>::QS;
   constexpr int NI = SchurCfg<N>::NI;
   auto& sc = F.s;
   const int t = threadIdx.x, q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
@@ -244,10 +266,11 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   if (iv)
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
-      sc.BL[i][j] = bl[j];
+      F.Bm[i][j] = bl[j];
       sc.VW[i][j] = vw[j];
     }
   wave_sync();
+  mark(13);
   // S = I + L'CL, row i in absolute column order (pads: identity).  S[i][m] is computed as the
   // same dot products in the same order by lanes i and m, so S is exactly symmetric.
   double S[64];
@@ -273,55 +296,49 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   // matrix X has X[p][j] = X[j][p] for j >= p and X[p][j] = -X[j][p] for j < p, so row p is lane
   // j's own column p with a sign: each pivot makes four 16-lane row copies of it with the
   // row-swap permutes and every lane applies X[t][j] += X[p][j] g_t with row_newbcast FMAs.
-  const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
+  mark(14);
   sfor<0, NI>([&](auto P) __attribute__((always_inline)) {
     constexpr int pv = decltype(P)::value;
     const double col = S[pv];
-    const double a0 = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(col), pv),
-                                       __builtin_amdgcn_readlane(__double2loint(col), pv));
-    const double pinv = recip(a0);
     const double rj = t < pv ? -col : col;
-    const double g = t == pv ? pinv - 1.0 : -(col * pinv);
-    const double newc = t == pv ? pinv : -(col * pinv);
-    // row p in every DPP row: copy s' (source row s') of lane (q, l) is rj of lane (s', l), the
-    // lane's own value when q == s', else its row-swap partner q ^ s'
-    const double r16 = xor16(rj), r32 = xor32(rj), r48 = xor32(r16);
-    // copy s' = the value of row q ^ (q ^ s'): bit 0 of q ^ s' picks the row-pair partner, bit 1
-    // the other pair (two levels of v_cndmask on the lane's row bits, no branches)
-    const double e0 = qb0 ? r16 : rj, e1 = qb0 ? rj : r16;    // rows {q, q^1} as seen from bit 0
-    const double f0 = qb0 ? r48 : r32, f1 = qb0 ? r32 : r48;  // rows {q^2, q^3}
-    const double x0 = qb1 ? f0 : e0, x1 = qb1 ? f1 : e1, x2 = qb1 ? e0 : f0, x3 = qb1 ? e1 : f1;
+    // row p of the current matrix in every DPP row, absolute column order (copy s' = columns
+    // 16 s' .. 16 s' + 15); the pivot X[p][p] is lane p & 15 of copy p >> 4
+    double x0, x1, x2, x3;
+    rowbcast4(rj, x0, x1, x2, x3);
+    const double xp = pv < 16 ? x0 : (pv < 32 ? x1 : (pv < 48 ? x2 : x3));
+    const double a0 = __builtin_amdgcn_update_dpp(0.0, xp, 0x150 + (pv & 15), 0xF, 0xF, false);
+    const double pinv = recip(a0);
+    const double cp = col * pinv;
+    const double g = t == pv ? pinv - 1.0 : -cp;
+    const double newc = t == pv ? pinv : -cp;
     upd16(x0, g, S);
     upd16(x1, g, S + 16);
     upd16(x2, g, S + 32);
     upd16(x3, g, S + 48);
     S[pv] = newc;
   });
-  // the lane's register factors, read back from the scratch (before Q overwrites it)
-#pragma unroll
-  for (int j = 0; j < 12; ++j) BR[j] = iv ? sc.BL[i][j] : 0.0;
+  mark(15);
+  // the lane's rows of R'^-1, read back from the scratch (before Q overwrites it)
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int kk = 4 * r + ig;
     const int kc = kk < N ? kk : N - 1;
-    const int col = 3 * leg + (av ? a : 2);
-#pragma unroll
-    for (int cc = 0; cc < 6; ++cc) BC[r][cc] = sc.BL[6 * kc + cc][col];
     const double* ri = sc.Ri[kc][leg] + 3 * (av ? a : 2);
     RI[r][0] = ri[0];
     RI[r][1] = ri[1];
     RI[r][2] = ri[2];
   }
   wave_sync();
-  // Q = I - S^-1 (pads and columns >= NI: 0)
+  // Q = I - S^-1 (columns NI .. QS-1: 0; the last row's tail: 0)
   if (iv) {
 #pragma unroll
-    for (int m = 0; m < 64; m += 2) {
+    for (int m = 0; m < QS; m += 2) {
       const double q0 = m < NI ? (t == m ? 1.0 : 0.0) - S[m] : 0.0;
       const double q1 = m + 1 < NI ? (t == m + 1 ? 1.0 : 0.0) - S[m + 1] : 0.0;
-      *reinterpret_cast<double2*>(&F.Q[i][m]) = make_double2(q0, q1);
+      *reinterpret_cast<double2*>(&F.Q[QS * i + m]) = make_double2(q0, q1);
     }
   }
+  if (t == 0) *reinterpret_cast<double2*>(&F.Q[QS * NI]) = make_double2(0.0, 0.0);
   wave_sync();
 }
 
@@ -329,70 +346,80 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
 // W[r]: w = D^-1 rhs in the variable layout; returns U[r] = (c B6'M B6 + R')^-1 w.
 template <int N, int R>
 __device__ __forceinline__ void schur_solve(SchurLds<N>& F, const double (&W)[R], const double (&RI)[R][3],
-                                            const double (&BC)[R][6], const double (&BR)[12], const bool (&vvr)[R],
-                                            double (&U)[R]) {
-  constexpr int NI = SchurCfg<N>::NI;
+                                            const bool (&vvr)[R], double (&U)[R]) {
+  constexpr int NI = SchurCfg<N>::NI, QS = SchurCfg<N>::QS, BS = SchurCfg<N>::BS;
   const int t = threadIdx.x, q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
   const bool av = a < 3;
   const int ig = gray(q);
   const int idx = 3 * leg + (av ? a : 2);
+  const int i = t < NI ? t : NI - 1;
+  const int k = i / 6;
+  // Q is constant between factorizations: its first two 16-column chunks are loaded before
+  // anything else (sched_barrier keeps the scheduler from sinking them to their use)
+  const double2* qr2 = reinterpret_cast<const double2*>(F.Q + QS * i);
+  double c0[16], c1[16];
+  auto load = [&](double (&c)[16], int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const double2 v = qr2[8 * s + e];
+      c[2 * e] = v.x;
+      c[2 * e + 1] = v.y;
+    }
+  };
+  load(c0, 0);
+  load(c1, 1);
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int r = 0; r < R; ++r)
     if (vvr[r]) F.wv[12 * (4 * r + ig) + idx] = W[r];
   wave_sync();
-  // impulse role: z = B w of the lane's step, then q = Q z
-  const int i = t < NI ? t : NI - 1;
-  const int k = i / 6;
-  double z = 0.0;
+  // impulse role: z = B w of the lane's step (its row of B from LDS)
+  double z;
   {
     const double2* w2 = reinterpret_cast<const double2*>(&F.wv[12 * k]);
+    const double2* b2 = reinterpret_cast<const double2*>(F.Bm[i]);
     double za = 0.0, zb = 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      const double2 v = w2[j];
-      za = fma(BR[2 * j], v.x, za);
-      zb = fma(BR[2 * j + 1], v.y, zb);
+      const double2 v = w2[j], bb = b2[j];
+      za = fma(bb.x, v.x, za);
+      zb = fma(bb.y, v.y, zb);
     }
     z = t < NI ? za + zb : 0.0;
   }
-  const double z1 = xor16(z), z2 = xor32(z), z3 = xor32(z1);
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  {
-    const double* qr = F.Q[i];
-    double c[16];
-    auto load = [&](int s) __attribute__((always_inline)) {
-      const double2* p2 = reinterpret_cast<const double2*>(qr + 16 * (q ^ s));
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const double2 v = p2[e];
-        c[2 * e] = v.x;
-        c[2 * e + 1] = v.y;
-      }
-    };
-    load(0);
-    mv16(z, c, a0, a1, a2, a3);
-    load(1);
-    mv16(z1, c, a0, a1, a2, a3);
-    load(2);
-    mv16(z2, c, a0, a1, a2, a3);
-    load(3);
-    mv16(z3, c, a0, a1, a2, a3);
-  }
-  const double qi = (a0 + a1) + (a2 + a3);
-  if (t < NI) F.qv[t] = qi;
-  wave_sync();
-  // variable role: u = R'^-1 w - B' q
+  // variable role: R'^-1 w of the lane's foot (independent of the dense product below)
+  double r1[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int kk = 4 * r + ig;
     const int kc = kk < N ? kk : N - 1;
     const double* wf = &F.wv[12 * kc + 3 * leg];
-    const double r1 = (RI[r][0] * wf[0] + RI[r][1] * wf[1]) + RI[r][2] * wf[2];
+    r1[r] = (RI[r][0] * wf[0] + RI[r][1] * wf[1]) + RI[r][2] * wf[2];
+  }
+  // q = Q z: z in every DPP row (absolute order), 64 row_newbcast FMAs
+  double z0, z1, z2, z3;
+  rowbcast4(z, z0, z1, z2, z3);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  mv16(z0, c0, a0, a1, a2, a3);
+  load(c0, 2);
+  mv16(z1, c1, a0, a1, a2, a3);
+  load(c1, 3);
+  mv16(z2, c0, a0, a1, a2, a3);
+  mv16(z3, c1, a0, a1, a2, a3);
+  const double qi = (a0 + a1) + (a2 + a3);
+  if (t < NI) F.qv[t] = qi;
+  wave_sync();
+  // variable role: u = R'^-1 w - B' q (column idx of B_k from LDS)
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int kk = 4 * r + ig;
+    const int kc = kk < N ? kk : N - 1;
     const double2* q2 = reinterpret_cast<const double2*>(&F.qv[6 * kc]);
     const double2 qa = q2[0], qb = q2[1], qc = q2[2];
-    const double y = ((((BC[r][0] * qa.x + BC[r][1] * qa.y) + BC[r][2] * qb.x) + BC[r][3] * qb.y) + BC[r][4] * qc.x) +
-                     BC[r][5] * qc.y;
-    U[r] = r1 - y;
+    const double* bc = &F.Bm[6 * kc][idx];
+    const double y = ((((bc[0] * qa.x + bc[BS] * qa.y) + bc[2 * BS] * qb.x) + bc[3 * BS] * qb.y) + bc[4 * BS] * qc.x) +
+                     bc[5 * BS] * qc.y;
+    U[r] = r1[r] - y;
   }
 }
 

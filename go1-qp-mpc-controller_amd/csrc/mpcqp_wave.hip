@@ -390,10 +390,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   // Record values used after the setup image is recycled (the LDS union is rewritten by the
   // factorization) are pinned into registers: keep() hides their origin, so the compiler cannot
   // rematerialize them by reloading the (by then overwritten) LDS words.
-  double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS], mu = rec[MPCQP_REC_MU];
+  double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS];
   keep(dt);
   keep(mass);
-  keep(mu);
   Adisc A;
   {
     const double yaw = rec[MPCQP_REC_EULER + 2];
@@ -592,9 +591,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 
   // ---- 5. ADMM (osqp_solve) ------------------------------------------------------------------------
   auto& F = sm.u.f;
-  // KS = 1: the lane's rows / columns of the Schur-form factors (mpcqp_schur.h), set per rho
-  double SRI[KS == 1 ? R : 1][3], SBC[KS == 1 ? R : 1][6], SBR[12];
-  (void)SRI; (void)SBC; (void)SBR;
+  // KS = 1: the lane's rows of R'^-1 (mpcqp_schur.h), set per rho
+  double SRI[KS == 1 ? R : 1][3];
+  (void)SRI;
   double rho = rho0, rinv = 1. / rho0, pri_res = 0.0, dua_res = 0.0;
   int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
   bool need_factor = true;
@@ -638,7 +637,8 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       }
       wave_sync();
       if constexpr (KS == 0) factorize_mfma<N>(sm, p, A, cost_c, dtm);
-      else schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI, SBC, SBR);
+      else schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI,
+                              [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; });
       wave_sync();
       need_factor = false;
       WV_MARK(12);
@@ -652,7 +652,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       double W[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) W[r] = DI[r] * RHS[r];
-      schur_solve<N, R>(F, W, SRI, SBC, SBR, vvr, U);
+      schur_solve<N, R>(F, W, SRI, vvr, U);
     } else {
       // LDS operands are loaded one phase ahead of their use; sched_barrier keeps the scheduler from
       // sinking a prefetch back down to its consumer (counted lgkmcnt waits then cover only it).
@@ -1066,8 +1066,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     if (t == 0) {
       ws[WL::FLAG] = 1.0;
       ws[WL::RHO] = rho;
-      ws[WL::C] = cost_c;
-      ws[WL::MU] = mu;
+      // c and mu reloaded from HBM here rather than carried through the loop (values live across
+      // the whole solve are the ones the register allocator parks in AGPRs / scratch)
+      ws[WL::C] = imv[SI::CS];
+      ws[WL::MU] = ((const volatile double*)(recs + (size_t)inst * C::REC))[MPCQP_REC_MU];
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {

@@ -36,6 +36,8 @@ def main():
             print(f"tick {t} ref iters {ref[t]['iters'].tolist()} rho_up {ref[t]['rho_updates'].tolist()} rho {np.round(ref[t]['rho'], 5).tolist()}")
             err = np.max(np.abs(g["u0"] - ref[t]["u0"]), axis=1)
             print(f"tick {t} |du0| {np.array2string(err, precision=2)}")
+            if t == 0:
+                np.save(os.environ.get("AB_SLOT_OUT", "/tmp/slot.npy"), st.cpu().numpy())
         w = st.cpu().numpy()
         print("slot flag/rho/c/mu", w[:, :4].tolist())
 

@@ -38,7 +38,8 @@ def main():
         torch.cuda.synchronize()
         marks = tr.cpu().numpy().reshape(a.traced, 64, 4)
         res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
-    ph = {k: [] for k in ("setup", "factor", "iter_cycles", "it_kkt", "it_update", "it_rest", "total", "shader_ghz")}
+    ph = {k: [] for k in ("setup", "factor", "f_pre", "f_buildS", "f_gj", "f_post", "iter_cycles", "it_kkt",
+                          "it_update", "it_rest", "total", "shader_ghz")}
     for b in range(a.traced):
         mk = marks[b]
         mk = mk[~np.isnan(mk[:, 0])]
@@ -50,6 +51,11 @@ def main():
         ph["setup"].append(at[4][0] - at[0][0])
         fac = [at[12][k] - at[10][k] for k in range(min(len(at[10]), len(at.get(12, []))))]
         ph["factor"] += fac
+        if 13 in at and 14 in at and 15 in at:  # Schur-form sub-phases (first factorization)
+            ph["f_pre"].append(at[13][0] - at[10][0])
+            ph["f_buildS"].append(at[14][0] - at[13][0])
+            ph["f_gj"].append(at[15][0] - at[14][0])
+            ph["f_post"].append(at[12][0] - at[15][0])
         ph["total"].append(at[20][0] - at[0][0])
         ph["iter_cycles"].append((at[20][0] - at[4][0] - sum(fac)) / max(int(res["iters"][b]), 1))
         if 40 in at and 45 in at:
