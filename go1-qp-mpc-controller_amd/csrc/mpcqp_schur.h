@@ -133,7 +133,11 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   constexpr int QS = SchurCfg<N>::QS;
   constexpr int NI = SchurCfg<N>::NI;
   auto& sc = F.s;
-  const int t = threadIdx.x, q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
+  // the lane id through an opaque copy: the per-lane masks derived from it (t == pivot, ...) are
+  // then computed here, not hoisted out of the ADMM loop into spilled registers
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  const int q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
   const bool av = a < 3;
   const int ig = gray(q);
   // R'^-1 per foot (cofactor inverse of the symmetric 3x3): the variable lane's row a
@@ -287,19 +291,21 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
       }
       const int mx = k > l ? k : l;
       const double s = (double)(N - mx) * dv + alpha_jl(N, k, l) * dw;
-      S[m] = iv ? (t == m ? 1.0 + s : s) : (t == m ? 1.0 : 0.0);
+      S[m] = iv ? s : 0.0;
     } else {
-      S[m] = t == m ? 1.0 : 0.0;
+      S[m] = 0.0;
     }
   }
-  // in-place Gauss-Jordan inverse of S (SPD: no pivoting).  With pivots 0..p-1 done, the current
+  // S holds L'CL so far: the identity is added to each diagonal entry when its pivot comes (entry
+  // (j, j) is read first by pivot j; the updates before it never read it) and pad rows stay 0.
+  // In-place Gauss-Jordan inverse of S (SPD: no pivoting).  With pivots 0..p-1 done, the current
   // matrix X has X[p][j] = X[j][p] for j >= p and X[p][j] = -X[j][p] for j < p, so row p is lane
   // j's own column p with a sign: each pivot makes four 16-lane row copies of it with the
   // row-swap permutes and every lane applies X[t][j] += X[p][j] g_t with row_newbcast FMAs.
   mark(14);
   sfor<0, NI>([&](auto P) __attribute__((always_inline)) {
     constexpr int pv = decltype(P)::value;
-    const double col = S[pv];
+    const double col = S[pv] + (t == pv ? 1.0 : 0.0);
     const double rj = t < pv ? -col : col;
     // row p of the current matrix in every DPP row, absolute column order (copy s' = columns
     // 16 s' .. 16 s' + 15); the pivot X[p][p] is lane p & 15 of copy p >> 4
@@ -329,14 +335,15 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
     RI[r][2] = ri[2];
   }
   wave_sync();
-  // Q = I - S^-1 (columns NI .. QS-1: 0; the last row's tail: 0)
+  // Q = I - S^-1 (columns NI .. QS-1: 0; the last row's tail: 0): -S^-1, then each row's diagonal
   if (iv) {
 #pragma unroll
     for (int m = 0; m < QS; m += 2) {
-      const double q0 = m < NI ? (t == m ? 1.0 : 0.0) - S[m] : 0.0;
-      const double q1 = m + 1 < NI ? (t == m + 1 ? 1.0 : 0.0) - S[m + 1] : 0.0;
+      const double q0 = m < NI ? -S[m] : 0.0;
+      const double q1 = m + 1 < NI ? -S[m + 1] : 0.0;
       *reinterpret_cast<double2*>(&F.Q[QS * i + m]) = make_double2(q0, q1);
     }
+    F.Q[QS * i + i] += 1.0;
   }
   if (t == 0) *reinterpret_cast<double2*>(&F.Q[QS * NI]) = make_double2(0.0, 0.0);
   wave_sync();
@@ -421,6 +428,76 @@ __device__ __forceinline__ void schur_solve(SchurLds<N>& F, const double (&W)[R]
                      bc[5 * BS] * qc.y;
     U[r] = r1[r] - y;
   }
+}
+
+// ---- P~v (termination checks, dual-infeasibility test, objective) --------------------------------
+// out = c D H (D v) with H = B6' M B6 + R (2 R on the diagonal), computed directly like OSQP's
+// update_info mat_vec (osqp auxil.c; oracle/mpc_oracle.c:760) instead of being carried through the
+// iterations: z = B6 (D v) on the impulse lanes, M z, then B6' (M z) + R D v on the variable lanes.
+// DVv[r] = D v and Dd[r] = D in the variable layout.  Uses wv / qv (not Q or B).
+template <int N, int R, class SM>
+__device__ __forceinline__ void schur_px(const SM& sm, SchurLds<N>& F, const mpcqp_params& p, const Adisc& A,
+                                         double dtm, double cost_c, const double (&DVv)[R], const double (&Dd)[R],
+                                         const bool (&vvr)[R], double (&out)[R]) {
+  constexpr int NI = SchurCfg<N>::NI;
+  const int t = threadIdx.x, q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
+  const bool av = a < 3;
+  const int ig = gray(q);
+  const int idx = 3 * leg + (av ? a : 2);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (vvr[r]) F.wv[12 * (4 * r + ig) + idx] = DVv[r];
+  wave_sync();
+  // impulse role, lane i = 6 k + c: z = B6_k (D v)_k (rows 0-2: B_w, rows 3-5: dt/m leg sums)
+  const int i = t < NI ? t : NI - 1, k = i / 6, c = i % 6;
+  {
+    const double* w = &F.wv[12 * k];
+    const double* bw = sm.Bw[k][c < 3 ? c : 0];
+    double zw = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) zw += bw[j] * w[j];
+    const int cc = c < 3 ? 0 : c - 3;
+    const double zv = dtm * (((w[cc] + w[3 + cc]) + w[6 + cc]) + w[9 + cc]);
+    F.qv[t] = t < NI ? (c < 3 ? zw : zv) : 0.0;
+  }
+  wave_sync();
+  // (M z)_(k,c) = Qv_c sum_l beta_kl z_(l,c) + (Ac6' Qp Ac6 sum_l alpha_kl z_l)_c
+  double mz;
+  {
+    double s1 = 0.0, s2[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int l = 0; l < N; ++l) {
+      const double* zl = &F.qv[6 * l];
+      const double al = alpha_jl(N, k, l), be = (double)(N - (k > l ? k : l));
+      s1 += be * zl[c];
+#pragma unroll
+      for (int f = 0; f < 6; ++f) s2[f] += al * zl[f];
+    }
+    // w_e = 2 q_e (Ac6 s2)_e; Ac6 = A[0:6, 6:12]
+    const double w0 = (2.0 * p.q_weights[0]) * (A.ad0 * s2[0] + A.ad1 * s2[1]);
+    const double w1 = (2.0 * p.q_weights[1]) * ((-A.ad1) * s2[0] + A.ad0 * s2[1]);
+    double wc = 0.0;
+#pragma unroll
+    for (int e = 2; e < 6; ++e) wc = c == e ? (2.0 * p.q_weights[e]) * (A.dt * s2[e]) : wc;
+    // (Ac6' w)_c: c = 0, 1 mix the yaw rotation; c = 2: dt w_2; c >= 3: dt w_c
+    const double ac = c == 0 ? A.ad0 * w0 + (-A.ad1) * w1 : (c == 1 ? A.ad1 * w0 + A.ad0 * w1 : A.dt * wc);
+    mz = (2.0 * p.q_weights[6 + c]) * s1 + ac;
+  }
+  wave_sync();
+  if (t < NI) F.qv[t] = mz;
+  wave_sync();
+  // variable role: (B6' M z)_j + 2 r_j (D v)_j, times c D
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int kk = 4 * r + ig;
+    const int kc = kk < N ? kk : N - 1;
+    const double* mk = &F.qv[6 * kc];
+    const double hv = ((((sm.Bw[kc][0][idx] * mk[0] + sm.Bw[kc][1][idx] * mk[1]) + sm.Bw[kc][2][idx] * mk[2]) +
+                        dtm * mk[3 + (av ? a : 2)]) +
+                       (2.0 * p.r_weights[idx]) * DVv[r]);
+    out[r] = vvr[r] ? (cost_c * Dd[r]) * hv : 0.0;
+  }
+  wave_sync();
 }
 
 }  // namespace wv

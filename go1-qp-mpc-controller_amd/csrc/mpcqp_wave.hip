@@ -321,16 +321,32 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
 // Phase timing (debug builds with -DMPCQP_PHASE_TIMING): lane 0 of each traced robot appends
 // {phase id, s_memtime, s_memrealtime (100 MHz), 0} to the trace buffer instead of check records.
 #ifdef MPCQP_PHASE_TIMING
+// MPCQP_PHASE_TIMING_ENDS: only the first and last marks (0, 20), with the wave's HW_ID register in
+// the fourth word, for per-robot durations and the dispatch timeline at no cost to the solve itself
+#ifdef MPCQP_PHASE_TIMING_ENDS
+#define WV_MARK_ON(id) ((id) == 0 || (id) == 20)
+// HW_ID (hwreg 4: wave, SIMD, CU, SE fields) + 2^32 XCC_ID (hwreg 20)
+#define WV_HWID()                                                          \
+  ((double)(unsigned)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)) + \
+   4294967296.0 * (double)(unsigned)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)))
+#else
+#define WV_MARK_ON(id) true
+#define WV_HWID() 0.0
+#endif
 #define WV_MARK(id)                                                                     \
   do {                                                                                  \
-    if (trace && threadIdx.x == 0 && inst < trace_cap && nmark < MPCQP_TRACE_LEN) {     \
+    if (WV_MARK_ON(id) && trace && threadIdx.x == 0 && inst < trace_cap && nmark < MPCQP_TRACE_LEN) { \
       double* tm_ = trace + ((size_t)inst * MPCQP_TRACE_LEN + nmark) * 4;                \
       tm_[0] = (id);                                                                    \
       tm_[1] = (double)__builtin_readcyclecounter();                                    \
       tm_[2] = (double)__builtin_amdgcn_s_memrealtime();                                \
+      tm_[3] = WV_HWID();                                                               \
       ++nmark;                                                                          \
     }                                                                                   \
   } while (0)
+#elif defined(MPCQP_ISA_MARKS)
+// static ISA accounting (tools/isa_phases.py): an assembly comment per phase mark
+#define WV_MARK(id) asm volatile(";WV_MARK %0" ::"n"(id))
 #else
 #define WV_MARK(id) \
   do {              \
@@ -522,7 +538,15 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     RI4[r] = 1. / RHO4[r];
   }
   if (mode != 0) {
-    // P~x of the warm iterate (the loop carries P~x through the KKT identity from here):
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      // compute_rhs from the warm x, z, y: sigma x - q~ + A~'(rho z - y)
+      const double at = quad_at(rho0 * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
+      RHS[r] = vvr[r] ? (sigma * X[r] - Qv[r]) + at : 0.0;
+    }
+  }
+  if (KS == 0 && mode != 0) {
+    // P~x of the warm iterate (the Riccati variant carries P~x through the KKT identity from here):
     // P~x = c D H (D x), H v = B_qp' Q B_qp v + R v by the dynamics: x_{i+1} = A x_i + B_i v_i
     // from x_0 = 0, e_i = Q x_{i+1}, lambda_j = e_j + A' lambda_{j+1}, (H v)_j = B_j' lambda_j + R v_j.
 #pragma unroll
@@ -564,9 +588,6 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       const double hv = (((sm.Bw[k][0][idx] * lm[6] + sm.Bw[k][1][idx] * lm[7]) + sm.Bw[k][2][idx] * lm[8]) +
                          dtm * lm[9 + idx % 3]) + (2 * p.r_weights[idx]) * HS.Dt[ND * k + idx];
       PX[r] = vvr[r] ? (c_s * Dv[r]) * hv : 0.0;
-      // compute_rhs from the warm x, z, y: sigma x - q~ + A~'(rho z - y)
-      const double at = quad_at(rho0 * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
-      RHS[r] = vvr[r] ? (sigma * X[r] - Qv[r]) + at : 0.0;
     }
   }
   // D and E of the lane's variable / rows, reloaded from the image (volatile: never hoisted into
@@ -594,6 +615,18 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   // KS = 1: the lane's rows of R'^-1 (mpcqp_schur.h), set per rho
   double SRI[KS == 1 ? R : 1][3];
   (void)SRI;
+  // KS = 1: P~v computed directly where the checks need it (mpcqp_schur.h schur_px)
+  auto px_of = [&](const double (&v)[R], double (&out)[R]) __attribute__((always_inline)) {
+    if constexpr (KS == 1) {
+      double dd[R], dvv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        dd[r] = dv_of(r);
+        dvv[r] = dd[r] * v[r];
+      }
+      schur_px<N, R>(sm, F, p, A, dtm, cost_c, dvv, dd, vvr, out);
+    }
+  };
   double rho = rho0, rinv = 1. / rho0, pri_res = 0.0, dua_res = 0.0;
   int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
   bool need_factor = true;
@@ -860,15 +893,17 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         Y4[r] = Y4[r] + dyv;
         if constexpr (info) DY4[r] = dyv;
       }
-      const double kd = quad_at(rho * zt, RHO4[r] * zt4, AK0[r], AK1[r], AK4[r], a);
       // every lane updates (values of padding lanes / steps past N are never read unmasked)
       const double xo = X[r];
       const double xn = alpha * xt + (1.0 - alpha) * xo;
       if constexpr (info) DX[r] = xn - xo;
       X[r] = xn;
-      const double pxt = (RHS[r] - sigma * xt) - kd;
-      if constexpr (info) PXO[r] = PX[r];
-      PX[r] = alpha * pxt + (1.0 - alpha) * PX[r];
+      if constexpr (KS == 0) {  // the Riccati variant carries P~x; the Schur form computes it at checks
+        const double kd = quad_at(rho * zt, RHO4[r] * zt4, AK0[r], AK1[r], AK4[r], a);
+        const double pxt = (RHS[r] - sigma * xt) - kd;
+        if constexpr (info) PXO[r] = PX[r];
+        PX[r] = alpha * pxt + (1.0 - alpha) * PX[r];
+      }
       // next right-hand side sigma x - q~ + A~'(rho z - y), here so that it interleaves with the other
       // rounds' updates (recomputed below when adapt_rho changes rho)
       const double at = quad_at(rho * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
@@ -881,6 +916,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     if (tm_it) WV_MARK(46);
     if (need_info) {
       // ---- update_info / check_termination / adapt_rho (osqp.c, auxil.c) ----
+      if constexpr (KS == 1) px_of(X, PX);
       double mx[14];
 #pragma unroll
       for (int k = 0; k < 14; ++k) mx[k] = 0.0;
@@ -978,10 +1014,13 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
           if (ndx > DIV_TOL) {
             qd = wave_sum(qd);
             if (qd < cost_c * eps_dinf * ndx) {
-              double pd = 0.0;
+              double pd = 0.0, PDX[R];
+              if constexpr (KS == 1) px_of(DX, PDX);
 #pragma unroll
-              for (int r = 0; r < R; ++r)
-                if (vvr[r]) pd = dmax(pd, dabs(DI[r] * (PX[r] - PXO[r])));
+              for (int r = 0; r < R; ++r) {
+                if constexpr (KS == 0) PDX[r] = PX[r] - PXO[r];
+                if (vvr[r]) pd = dmax(pd, dabs(DI[r] * PDX[r]));
+              }
               pd = wave_max(pd);
               if (pd < cost_c * eps_dinf * ndx) {
                 double viol = 0.0;
@@ -1102,7 +1141,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                        status != MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE &&
                        status != MPCQP_STATUS_DUAL_INFEASIBLE &&
                        status != MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE && status != MPCQP_STATUS_NON_CVX;
-  double ob = 0.0;
+  double ob = 0.0;  // (the loop always ends on a need_info iteration: PX is P~x of the final x)
 #pragma unroll
   for (int r = 0; r < R; ++r)
     if (vvr[r]) ob += 0.5 * X[r] * PX[r] + Qv[r] * X[r];

@@ -1,6 +1,12 @@
-set -e
+# SQ counters of wave_kernel (one --pmc pass per call, each under its own time limit)
+#   tools/pmc_sq.sh OUTDIR "COUNTERS..." [bench args]
+set -euo pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r2pmc
-mkdir -p $O
-timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-include-regex wave_kernel --output-format csv -d $O/a -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $O/a.out 2> $O/a.err
+O=$1
+CTR=$2
+shift 2
+mkdir -p "$O"
+[ -f "$O/counters.txt" ] || timeout -s KILL 60 rocprofv3 -L > "$O/counters.txt" 2>&1 || true
+tag=$(echo "$CTR" | tr ' ' '_' | cut -c1-60)
+timeout -s KILL 120 rocprofv3 --pmc $CTR --kernel-include-regex wave_kernel --output-format csv -d "$O/$tag" -o pmc \
+  -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-extras "$@" > "$O/$tag.out" 2> "$O/$tag.err"
