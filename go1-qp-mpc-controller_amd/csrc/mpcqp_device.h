@@ -128,17 +128,51 @@ __device__ __forceinline__ double xor32(double v) {
   const bool upper = (threadIdx.x >> 5) & 1;
   return __hiloint2double((int)(upper ? h2[0] : h2[1]), (int)(upper ? l2[0] : l2[1]));
 }
+// Row-pair / row-half combine for commutative all-reduces: permlane16_swap(v, v) leaves rows
+// [r0 r0 r2 r2] in one copy and [r1 r1 r3 r3] in the other (permlane32_swap likewise for the halves),
+// so op(copy0, copy1) is the pair's result in every lane with no lane select, bitwise the same in
+// both partners.
+template <class Op>
+__device__ __forceinline__ double swap16_reduce(double v, Op op) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto l2 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h2 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return op(__hiloint2double((int)h2[0], (int)l2[0]), __hiloint2double((int)h2[1], (int)l2[1]));
+}
+template <class Op>
+__device__ __forceinline__ double swap32_reduce(double v, Op op) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return op(__hiloint2double((int)h2[0], (int)l2[0]), __hiloint2double((int)h2[1], (int)l2[1]));
+}
 __device__ __forceinline__ double wave_max(double v) {
+  auto op = [](double a, double b) __attribute__((always_inline)) { return dmax(a, b); };
   v = g16_max(v);
-  v = dmax(v, xor16(v));
-  v = dmax(v, xor32(v));
-  return v;
+  v = swap16_reduce(v, op);
+  return swap32_reduce(v, op);
 }
 __device__ __forceinline__ double wave_sum(double v) {
+  auto op = [](double a, double b) __attribute__((always_inline)) { return a + b; };
   v = g16_sum(v);
-  v = v + xor16(v);
-  v = v + xor32(v);
-  return v;
+  v = swap16_reduce(v, op);
+  return swap32_reduce(v, op);
+}
+// max of two non-negative, non-NaN doubles (norms of absolute values), where fmax equals dmax
+// bitwise: one v_max_f64, without the IEEE-mode canonicalization the compiler wraps around fmax
+__device__ __forceinline__ double nmax(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double wave_nmax(double v) {
+  auto op = [](double a, double b) __attribute__((always_inline)) { return nmax(a, b); };
+  v = nmax(v, dpp<0x140>(v));
+  v = nmax(v, dpp<0x141>(v));
+  v = nmax(v, dpp<0x4E>(v));
+  v = nmax(v, dpp<0xB1>(v));
+  v = swap16_reduce(v, op);
+  return swap32_reduce(v, op);
 }
 
 // ---- condensation: ConvexMpc.cpp:110-245 ----------------------------------------------------

@@ -98,6 +98,29 @@ __device__ __forceinline__ void upd16(double x, double g, double* s) {
       : [x] "v"(x), [g] "v"(g));
 }
 #undef SC_U
+// s[e] += bcast_(O+e)(x) * g for e < 4: a quarter of upd16, so that other work can be scheduled
+// between the quarters (s_nop 1: x may have been written by VALU just before)
+#define SC_U4(A, L) "v_fmac_f64_dpp %[" A "], %[x], %[g] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#define SC_DEF_UPD4(O, L0, L1, L2, L3)                                                               \
+  __device__ __forceinline__ void upd4_##O(double x, double g, double* s) {                          \
+    asm("s_nop 1\n\t" SC_U4("s0", L0) SC_U4("s1", L1) SC_U4("s2", L2) SC_U4("s3", L3)              \
+        : [s0] "+v"(s[0]), [s1] "+v"(s[1]), [s2] "+v"(s[2]), [s3] "+v"(s[3])                        \
+        : [x] "v"(x), [g] "v"(g));                                                                   \
+  }
+SC_DEF_UPD4(0, 0, 1, 2, 3)
+SC_DEF_UPD4(4, 4, 5, 6, 7)
+SC_DEF_UPD4(8, 8, 9, 10, 11)
+SC_DEF_UPD4(12, 12, 13, 14, 15)
+#undef SC_DEF_UPD4
+#undef SC_U4
+// columns 16 C .. 16 C + 15 of the lane's row s (those below NI: pad columns stay 0)
+template <int C, int NI>
+__device__ __forceinline__ void upd_chunk(double x, double g, double* s) {
+  if constexpr (16 * C + 0 < NI) upd4_0(x, g, s + 16 * C + 0);
+  if constexpr (16 * C + 4 < NI) upd4_4(x, g, s + 16 * C + 4);
+  if constexpr (16 * C + 8 < NI) upd4_8(x, g, s + 16 * C + 8);
+  if constexpr (16 * C + 12 < NI) upd4_12(x, g, s + 16 * C + 12);
+}
 
 // Row broadcasts: c_s = the value DPP row s holds, in every DPP row (lane l of each row gets lane
 // l of row s).  permlane16_swap(v, v) gives [r0 r0 r2 r2] / [r1 r1 r3 r3] (rows 0..3), and a
@@ -303,25 +326,40 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   // j's own column p with a sign: each pivot makes four 16-lane row copies of it with the
   // row-swap permutes and every lane applies X[t][j] += X[p][j] g_t with row_newbcast FMAs.
   mark(14);
-  sfor<0, NI>([&](auto P) __attribute__((always_inline)) {
+  // Software-pipelined: the chunk holding the next pivot's column is updated first, then the next
+  // pivot's row broadcast and reciprocal (a long dependent chain) are issued among the other chunks'
+  // independent FMAs.  Pad columns (>= NI) are skipped: their row entries are all zero.
+  struct Piv {
+    double x[4], g, newc;
+  };
+  auto prelude = [&](auto P) __attribute__((always_inline)) {
     constexpr int pv = decltype(P)::value;
+    Piv o;
     const double col = S[pv] + (t == pv ? 1.0 : 0.0);
     const double rj = t < pv ? -col : col;
     // row p of the current matrix in every DPP row, absolute column order (copy s' = columns
     // 16 s' .. 16 s' + 15); the pivot X[p][p] is lane p & 15 of copy p >> 4
-    double x0, x1, x2, x3;
-    rowbcast4(rj, x0, x1, x2, x3);
-    const double xp = pv < 16 ? x0 : (pv < 32 ? x1 : (pv < 48 ? x2 : x3));
-    const double a0 = __builtin_amdgcn_update_dpp(0.0, xp, 0x150 + (pv & 15), 0xF, 0xF, false);
+    rowbcast4(rj, o.x[0], o.x[1], o.x[2], o.x[3]);
+    const double a0 = __builtin_amdgcn_update_dpp(0.0, o.x[pv >> 4], 0x150 + (pv & 15), 0xF, 0xF, false);
     const double pinv = recip(a0);
     const double cp = col * pinv;
-    const double g = t == pv ? pinv - 1.0 : -cp;
-    const double newc = t == pv ? pinv : -cp;
-    upd16(x0, g, S);
-    upd16(x1, g, S + 16);
-    upd16(x2, g, S + 32);
-    upd16(x3, g, S + 48);
-    S[pv] = newc;
+    o.g = t == pv ? pinv - 1.0 : -cp;
+    o.newc = t == pv ? pinv : -cp;
+    return o;
+  };
+  Piv cur = prelude(IC<0>{});
+  sfor<0, NI>([&](auto P) __attribute__((always_inline)) {
+    constexpr int pv = decltype(P)::value;
+    constexpr int cs = (pv + 1 < NI ? pv + 1 : pv) >> 4;
+    upd_chunk<cs, NI>(cur.x[cs], cur.g, S);
+    Piv nxt;
+    if constexpr (pv + 1 < NI) nxt = prelude(IC<pv + 1>{});
+    if constexpr (cs != 0) upd_chunk<0, NI>(cur.x[0], cur.g, S);
+    if constexpr (cs != 1) upd_chunk<1, NI>(cur.x[1], cur.g, S);
+    if constexpr (cs != 2) upd_chunk<2, NI>(cur.x[2], cur.g, S);
+    if constexpr (cs != 3) upd_chunk<3, NI>(cur.x[3], cur.g, S);
+    S[pv] = cur.newc;
+    if constexpr (pv + 1 < NI) cur = nxt;
   });
   mark(15);
   // the lane's rows of R'^-1, read back from the scratch (before Q overwrites it)

@@ -592,7 +592,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   }
   // D and E of the lane's variable / rows, reloaded from the image (volatile: never hoisted into
   // loop-carried registers)
-  const volatile double* imv = im;
+  // (a global-address-space pointer: global_load, not flat_load, whose lgkmcnt share would also
+  // wait on the LDS traffic in flight)
+  using gvd = const volatile __attribute__((address_space(1))) double;
+  gvd* imv = (gvd*)im;
   auto dv_of = [&](int r) __attribute__((always_inline)) {
     return vvr[r] ? imv[SI::D + ND * (4 * r + ig) + idx] : 1.0;
   };
@@ -633,6 +636,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
   for (int iter = 1; iter <= p.max_iter; ++iter) {
     if (need_factor) {
+#ifdef MPCQP_REPEAT_FACTOR  // cost measurement builds: the (idempotent) factorization runs twice
+     for (int rep = 0; rep < 2; ++rep) {
+#endif
       WV_MARK(10);
       // R'_k foot blocks: c 2r + D^-1 (sigma I + A~' diag(rho) A~) D^-1
 #pragma unroll
@@ -673,6 +679,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       else schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI,
                               [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; });
       wave_sync();
+#ifdef MPCQP_REPEAT_FACTOR
+     }
+#endif
       need_factor = false;
       WV_MARK(12);
     }
@@ -686,6 +695,14 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 #pragma unroll
       for (int r = 0; r < R; ++r) W[r] = DI[r] * RHS[r];
       schur_solve<N, R>(F, W, SRI, vvr, U);
+#ifdef MPCQP_REPEAT_SOLVE  // cost measurement builds: the (idempotent) KKT solve runs twice
+      {
+        double W2[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) W2[r] = W[r] + 0.0 * U[r];  // after the first solve
+        schur_solve<N, R>(F, W2, SRI, vvr, U);
+      }
+#endif
     } else {
       // LDS operands are loaded one phase ahead of their use; sched_barrier keeps the scheduler from
       // sinking a prefetch back down to its consumer (counted lgkmcnt waits then cover only it).
@@ -926,29 +943,29 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         const double ax = AK0[r] * xp + AK1[r] * xz, ax4 = AK4[r] * xz;
         const double aty = quad_at(Y[r], Y4[r], AK0[r], AK1[r], AK4[r], a);
         if (kvr[r]) {
-          const double ei = 1.0 / ev_of(r), ei4 = 1.0 / e4_of(r);
+          const double ei = recip(ev_of(r)), ei4 = recip(e4_of(r));
           const double pr = ax + (-1.0) * Z[r], pr4 = ax4 + (-1.0) * Z4[r];
-          mx[0] = dmax(mx[0], dmax(dabs(ei * pr), dabs(ei4 * pr4)));
-          mx[1] = dmax(mx[1], dmax(dabs(pr), dabs(pr4)));
-          mx[2] = dmax(mx[2], dmax(dabs(ei * Z[r]), dabs(ei4 * Z4[r])));
-          mx[3] = dmax(mx[3], dmax(dabs(Z[r]), dabs(Z4[r])));
-          mx[4] = dmax(mx[4], dmax(dabs(ei * ax), dabs(ei4 * ax4)));
-          mx[5] = dmax(mx[5], dmax(dabs(ax), dabs(ax4)));
+          mx[0] = nmax(mx[0], nmax(dabs(ei * pr), dabs(ei4 * pr4)));
+          mx[1] = nmax(mx[1], nmax(dabs(pr), dabs(pr4)));
+          mx[2] = nmax(mx[2], nmax(dabs(ei * Z[r]), dabs(ei4 * Z4[r])));
+          mx[3] = nmax(mx[3], nmax(dabs(Z[r]), dabs(Z4[r])));
+          mx[4] = nmax(mx[4], nmax(dabs(ei * ax), dabs(ei4 * ax4)));
+          mx[5] = nmax(mx[5], nmax(dabs(ax), dabs(ax4)));
         }
         if (vvr[r]) {
           const double d = (Qv[r] + 1.0 * PX[r]) + 1.0 * aty;
-          mx[6] = dmax(mx[6], dabs(DI[r] * d));
-          mx[7] = dmax(mx[7], dabs(d));
-          mx[8] = dmax(mx[8], dabs(DI[r] * Qv[r]));
-          mx[9] = dmax(mx[9], dabs(Qv[r]));
-          mx[10] = dmax(mx[10], dabs(DI[r] * aty));
-          mx[11] = dmax(mx[11], dabs(aty));
-          mx[12] = dmax(mx[12], dabs(DI[r] * PX[r]));
-          mx[13] = dmax(mx[13], dabs(PX[r]));
+          mx[6] = nmax(mx[6], dabs(DI[r] * d));
+          mx[7] = nmax(mx[7], dabs(d));
+          mx[8] = nmax(mx[8], dabs(DI[r] * Qv[r]));
+          mx[9] = nmax(mx[9], dabs(Qv[r]));
+          mx[10] = nmax(mx[10], dabs(DI[r] * aty));
+          mx[11] = nmax(mx[11], dabs(aty));
+          mx[12] = nmax(mx[12], dabs(DI[r] * PX[r]));
+          mx[13] = nmax(mx[13], dabs(PX[r]));
         }
       }
 #pragma unroll
-      for (int k = 0; k < 14; ++k) mx[k] = wave_max(mx[k]);
+      for (int k = 0; k < 14; ++k) mx[k] = wave_nmax(mx[k]);
       pri_res = mx[0];
       dua_res = cinv * mx[6];
       iters = iter;
@@ -979,12 +996,12 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
             dyp[r] = d;
             dyp4[r] = d4;
             if (kvr[r]) {
-              nd = dmax(nd, dmax(dabs(evr * d), dabs(e4r * d4)));
+              nd = nmax(nd, nmax(dabs(evr * d), dabs(e4r * d4)));
               lh += hi * dmax(d, 0.0) + lo * dmin(d, 0.0);
               if (a == 0) lh += U4[r] * dmax(d4, 0.0) + L4[r] * dmin(d4, 0.0);
             }
           }
-          const double ndy = wave_max(nd);
+          const double ndy = wave_nmax(nd);
           if (ndy > DIV_TOL) {
             lh = wave_sum(lh);
             if (lh < eps_pinf * ndy) {
@@ -992,9 +1009,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 #pragma unroll
               for (int r = 0; r < R; ++r) {
                 const double atd = quad_at(dyp[r], dyp4[r], AK0[r], AK1[r], AK4[r], a);
-                if (vvr[r]) an = dmax(an, dabs(DI[r] * atd));
+                if (vvr[r]) an = nmax(an, dabs(DI[r] * atd));
               }
-              an = wave_max(an);
+              an = wave_nmax(an);
               prim_inf = an < eps_pinf * ndy;
             }
           }
@@ -1007,10 +1024,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 #pragma unroll
           for (int r = 0; r < R; ++r)
             if (vvr[r]) {
-              nx = dmax(nx, dabs(dv_of(r) * DX[r]));
+              nx = nmax(nx, dabs(dv_of(r) * DX[r]));
               qd += Qv[r] * DX[r];
             }
-          const double ndx = wave_max(nx);
+          const double ndx = wave_nmax(nx);
           if (ndx > DIV_TOL) {
             qd = wave_sum(qd);
             if (qd < cost_c * eps_dinf * ndx) {
@@ -1019,9 +1036,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 #pragma unroll
               for (int r = 0; r < R; ++r) {
                 if constexpr (KS == 0) PDX[r] = PX[r] - PXO[r];
-                if (vvr[r]) pd = dmax(pd, dabs(DI[r] * PDX[r]));
+                if (vvr[r]) pd = nmax(pd, dabs(DI[r] * PDX[r]));
               }
-              pd = wave_max(pd);
+              pd = wave_nmax(pd);
               if (pd < cost_c * eps_dinf * ndx) {
                 double viol = 0.0;
 #pragma unroll
@@ -1040,7 +1057,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                       viol = 1.0;
                   }
                 }
-                viol = wave_max(viol);
+                viol = wave_nmax(viol);
                 dual_inf = viol == 0.0;
               }
             }

@@ -551,7 +551,11 @@ struct ScaleCfg {
   static constexpr int BPT = (N + TPC - 1) / TPC;    // horizon blocks of the column per thread
   static constexpr int NTS = ((TPC * n + 63) / 64) * 64;
   static constexpr int NWS = NTS / 64;
+#ifdef MPCQP_SCALE_WPE
+  static constexpr int WPE = MPCQP_SCALE_WPE;
+#else
   static constexpr int WPE = NWS >= 2 ? NWS / 2 : 1;  // waves per SIMD for two robots per CU
+#endif
   static constexpr int RPT = (m + NTS - 1) / NTS;   // constraint rows per thread
 };
 

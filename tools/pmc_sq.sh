@@ -7,6 +7,6 @@ CTR=$2
 shift 2
 mkdir -p "$O"
 [ -f "$O/counters.txt" ] || timeout -s KILL 60 rocprofv3 -L > "$O/counters.txt" 2>&1 || true
-tag=$(echo "$CTR" | tr ' ' '_' | cut -c1-60)
-timeout -s KILL 120 rocprofv3 --pmc $CTR --kernel-include-regex wave_kernel --output-format csv -d "$O/$tag" -o pmc \
+tag=${KRE:-wave}_$(echo "$CTR" | tr ' ' '_' | cut -c1-60)
+timeout -s KILL 120 rocprofv3 --pmc $CTR --kernel-include-regex "${KRE:-wave_kernel}" --output-format csv -d "$O/$tag" -o pmc \
   -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-extras "$@" > "$O/$tag.out" 2> "$O/$tag.err"
