@@ -50,7 +50,6 @@ struct SchurScratch {
   alignas(16) double Ri[N][4][9];   // R'^-1 foot blocks, row-major
   alignas(16) double B6R[NI][12];   // rows of B6 R'^-1 (step k = i / 6)
   alignas(16) double G[N][36];      // G_k = B_k R'_k^-1 B_k' (row c written by lane 6k + c)
-  alignas(16) double VW[NI][12];    // columns of sqrt(c) Qv^1/2 L_k and sqrt(c) Qp^1/2 Ac6 L_k
 };
 
 template <int N>
@@ -122,6 +121,24 @@ __device__ __forceinline__ void upd_chunk(double x, double g, double* s) {
   if constexpr (16 * C + 12 < NI) upd4_12(x, g, s + 16 * C + 12);
 }
 
+// a_j = sum_e bcast_(Lj)(x[e]) * v[e] for four lanes Lj of x's DPP row, each an fma chain in e
+// order starting from 0 (so lanes i and m form the dot product of their vectors bitwise alike); the
+// four chains interleave, each accumulator re-read four instructions after its last write.
+#define SC_D(A, X, V, L) "v_fmac_f64_dpp %[" A "], %[" X "], %[" V "] row_newbcast:%[" L "] row_mask:0xf bank_mask:0xf\n\t"
+#define SC_D4(X, V) SC_D("a0", X, V, "l0") SC_D("a1", X, V, "l1") SC_D("a2", X, V, "l2") SC_D("a3", X, V, "l3")
+template <int L0, int L1, int L2, int L3>
+__device__ __forceinline__ void dot6x4(const double (&x)[6], const double (&v)[6], double& a0, double& a1, double& a2,
+                                       double& a3) {
+  asm("s_nop 1\n\t" SC_D4("x0", "v0") SC_D4("x1", "v1") SC_D4("x2", "v2") SC_D4("x3", "v3") SC_D4("x4", "v4")
+      SC_D4("x5", "v5")
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
+      : [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]),
+        [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]),
+        [l0] "n"(L0), [l1] "n"(L1), [l2] "n"(L2), [l3] "n"(L3));
+}
+#undef SC_D4
+#undef SC_D
+
 // Row broadcasts: c_s = the value DPP row s holds, in every DPP row (lane l of each row gets lane
 // l of row s).  permlane16_swap(v, v) gives [r0 r0 r2 r2] / [r1 r1 r3 r3] (rows 0..3), and a
 // permlane32_swap of each of those with itself gives [r0 x4] / [r2 x4] and [r1 x4] / [r3 x4].
@@ -172,7 +189,7 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
     const double m00 = m[0], m01 = m[1], m02 = m[2], m11 = m[3], m12 = m[4], m22 = m[5];
     const double c00 = m11 * m22 - m12 * m12, c01 = m02 * m12 - m01 * m22, c02 = m01 * m12 - m02 * m11;
     const double c11 = m00 * m22 - m02 * m02, c12 = m01 * m02 - m00 * m12, c22 = m00 * m11 - m01 * m01;
-    const double inv = 1.0 / ((m00 * c00 + m01 * c01) + m02 * c02);
+    const double inv = recip((m00 * c00 + m01 * c01) + m02 * c02);
     const double i0 = sel3(a, c00, c01, c02) * inv, i1 = sel3(a, c01, c11, c12) * inv,
                  i2 = sel3(a, c02, c12, c22) * inv;
     if (k < N && av) {
@@ -222,7 +239,7 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   }
   wave_sync();
   // Cholesky G_k = L L' and Li = L^-1 (every lane of the step, redundantly)
-  double L[6][6], Li[6][6];
+  double L[6][6], Li[6][6], Ldi[6];
 #pragma unroll
   for (int r2 = 0; r2 < 6; ++r2)
 #pragma unroll
@@ -232,8 +249,9 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
     double s = sc.G[k][6 * cc + cc];
 #pragma unroll
     for (int e = 0; e < cc; ++e) s -= L[cc][e] * L[cc][e];
-    const double dg = sqrt(s), dinv = 1.0 / dg;
+    const double dg = sqrt(s), dinv = recip(dg);
     L[cc][cc] = dg;
+    Ldi[cc] = dinv;
 #pragma unroll
     for (int r2 = cc + 1; r2 < 6; ++r2) {
       double v = sc.G[k][6 * r2 + cc];
@@ -253,7 +271,7 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
       double v = r2 == cc ? 1.0 : 0.0;
 #pragma unroll
       for (int e = cc; e < r2; ++e) v -= L[r2][e] * Li[e][cc];
-      Li[r2][cc] = v / L[r2][r2];
+      Li[r2][cc] = v * Ldi[r2];
     }
   }
   // the lane's column c of L and row c of Li (c is per lane: selects, not register indexing)
@@ -289,36 +307,44 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
     for (int f = 0; f < 6; ++f) s += A.at(e, 6 + f) * Lc[f];
     vw[6 + e] = sqrt(cost_c * (2.0 * p.q_weights[e])) * s;
   }
-  // sc.B6R is read above by every lane before any lane writes BL / VW (in-order LDS of one wave)
+  // sc.B6R is read above by every lane before any lane writes B (in-order LDS of one wave)
   if (iv)
 #pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      F.Bm[i][j] = bl[j];
-      sc.VW[i][j] = vw[j];
-    }
-  wave_sync();
+    for (int j = 0; j < 12; ++j) F.Bm[i][j] = bl[j];
+  // pad lanes: zero columns (their rows of S stay 0; nothing reads their broadcasts)
+#pragma unroll
+  for (int e = 0; e < 12; ++e) vw[e] = iv ? vw[e] : 0.0;
   mark(13);
-  // S = I + L'CL, row i in absolute column order (pads: identity).  S[i][m] is computed as the
-  // same dot products in the same order by lanes i and m, so S is exactly symmetric.
+  // S - I = L'CL = beta o (V V') + alpha o (W W') (V, W: the 6-column halves of vw; beta, alpha per
+  // step pair), row i in absolute column order, by row_newbcast dot products against four row
+  // copies of each column: no LDS.  Entry (i, m) is the same fma chains by lanes i and m and the
+  // same symmetric coefficients, so S is exactly symmetric.
   double S[64];
 #pragma unroll
-  for (int m = 0; m < 64; ++m) {
-    if (m < NI) {
-      const int l = m / 6;
-      const double* o = sc.VW[m];
-      double dv = 0.0, dw = 0.0;
+  for (int m = 0; m < 64; ++m) S[m] = 0.0;
+  sfor<0, 2>([&](auto PART) __attribute__((always_inline)) {
+    constexpr int part = decltype(PART)::value;
+    double xc[4][6], v6[6];
 #pragma unroll
-      for (int e = 0; e < 6; ++e) {
-        dv += vw[e] * o[e];
-        dw += vw[6 + e] * o[6 + e];
-      }
-      const int mx = k > l ? k : l;
-      const double s = (double)(N - mx) * dv + alpha_jl(N, k, l) * dw;
-      S[m] = iv ? s : 0.0;
-    } else {
-      S[m] = 0.0;
+    for (int e = 0; e < 6; ++e) {
+      v6[e] = vw[6 * part + e];
+      rowbcast4(v6[e], xc[0][e], xc[1][e], xc[2][e], xc[3][e]);
     }
-  }
+    sfor<0, (NI + 3) / 4>([&](auto B) __attribute__((always_inline)) {
+      constexpr int m0 = 4 * decltype(B)::value, sr = m0 >> 4, l0 = m0 & 15;
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      dot6x4<l0, l0 + 1, l0 + 2, l0 + 3>(xc[sr], v6, acc[0], acc[1], acc[2], acc[3]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + j;
+        if (m < NI) {
+          const int l = m / 6;
+          if constexpr (part == 0) S[m] = (double)(N - (k > l ? k : l)) * acc[j];
+          else S[m] = fma(alpha_jl(N, k, l), acc[j], S[m]);
+        }
+      }
+    });
+  });
   // S holds L'CL so far: the identity is added to each diagonal entry when its pivot comes (entry
   // (j, j) is read first by pivot j; the updates before it never read it) and pad rows stay 0.
   // In-place Gauss-Jordan inverse of S (SPD: no pivoting).  With pivots 0..p-1 done, the current
