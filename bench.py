@@ -255,9 +255,13 @@ def run_rank(args):
                 "bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS, "traffic": load_traffic(key, eff_name),
                 "kernel": eff_name, "kernel_ms": kern_ms, "algorithmic_flop_per_launch": flops,
-                "note": "binary64; the ADMM iterations run on the VALU (v_fmac_f64 DPP mat-vecs) and bound "
-                        "the solve, the Riccati factorization runs on v_mfma_f64_16x16x4f64; peak = FP64 "
-                        "vector spec (equal to the FP64 MFMA peak on gfx950)"}
+                "note": ("binary64 on the VALU (v_fmac_f64 DPP): "
+                         + ("impulse-space Schur-form KKT solve (one dense 6N x 6N mat-vec per ADMM "
+                            "iteration, in-register Gauss-Jordan per rho)" if N <= 10 else
+                            "Riccati-form KKT solve (chains of 12x12 mat-vecs per iteration, factorization "
+                            "on v_mfma_f64_16x16x4f64)")
+                         + "; FLOPs = SURVEY §8(d)'s structure-exploiting count per robot with its actual "
+                           "iterations and rho updates; peak = FP64 vector spec (= FP64 MFMA peak on gfx950)")}
             pyoracle = None
             if not args.no_cpu:
                 pyoracle = oracle_module()

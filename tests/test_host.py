@@ -146,7 +146,12 @@ def test_product_library_ships_only_the_default_solve():
         return out
     prod = kernels(_lib.LIB_PATH)
     dbg = kernels(_lib.DEBUG_LIB_PATH)
-    assert "mpcqp::wv::wave_kernel<10>" in prod and "mpcqp::wv::scale_kernel<10>" in prod
+    # horizon 10: the Schur-form solve (KS = 1) and the Riccati form (KS = 0, negative weights);
+    # horizon 20: Riccati only
+    for k in ("mpcqp::wv::wave_kernel<10, 1>", "mpcqp::wv::wave_kernel<10, 0>", "mpcqp::wv::wave_kernel<20, 0>",
+              "mpcqp::wv::scale_kernel<10>", "mpcqp::wv::scale_kernel<20>"):
+        assert k in prod, k
+    assert "mpcqp::wv::wave_kernel<20, 1>" not in prod
     for name in ("mpcqp::solve_kernel<", "mpcqp::ric::ric_solve_kernel<", "mw_kernel", "dx_kernel"):
         assert name not in prod, name
     assert "mpcqp::solve_kernel<10>" in dbg and "mpcqp::ric::ric_solve_kernel<10>" in dbg
