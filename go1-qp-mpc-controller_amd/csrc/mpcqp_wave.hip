@@ -1158,7 +1158,8 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                        status != MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE &&
                        status != MPCQP_STATUS_DUAL_INFEASIBLE &&
                        status != MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE && status != MPCQP_STATUS_NON_CVX;
-  double ob = 0.0;  // (the loop always ends on a need_info iteration: PX is P~x of the final x)
+  // (the loop always ends on a need_info iteration: P~x is that of the final x)
+  double ob = 0.0;
 #pragma unroll
   for (int r = 0; r < R; ++r)
     if (vvr[r]) ob += 0.5 * X[r] * PX[r] + Qv[r] * X[r];
