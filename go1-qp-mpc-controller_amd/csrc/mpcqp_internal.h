@@ -52,7 +52,7 @@ __host__ __device__ constexpr int warm_state_doubles(int N) {
 }
 
 // doubles per robot of the scaling image scale_kernel hands to wave_kernel (mpcqp_wave.hip ScaleImg)
-__host__ __device__ constexpr int scale_image_doubles(int N) { return 3 * 12 * N + 3 * 20 * N + 2; }
+__host__ __device__ constexpr int scale_image_doubles(int N) { return 3 * 12 * N + 20 * N + 2; }
 
 // Downstream torque map (mpcqp_torque.hip)
 hipError_t launch_torques(const double* recs, const mpcqp_result* grf, int batch, int* counter, double* tau,

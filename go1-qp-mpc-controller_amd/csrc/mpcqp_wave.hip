@@ -118,16 +118,19 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   constexpr int BPT = SC::BPT;
   const int j0 = t / SC::TPC, jb = (t % SC::TPC) * BPT;
   const bool lead = (t % SC::TPC) == 0;  // the lane that owns the column's per-column values
+  // D and E of the current pass (each pass writes the other buffer: no read-before-write barrier)
+  double* Dc = sm.D[0];
+  double* Ec = sm.E[0];
   if (lead && j0 < n) {
     const int k = j0 / ND, ii = j0 % ND;
     const double* lm = sm.lam[k];
     const double g = ((sm.Bw[k][0][ii] * lm[6] + sm.Bw[k][1][ii] * lm[7]) + sm.Bw[k][2][ii] * lm[8]) + dtm * lm[9 + ii % 3];
     sm.q[j0] = g;
     sm.qn[j0] = g;
-    sm.D[j0] = 1.0;
+    Dc[j0] = 1.0;
   }
   for (int r = t; r < m; r += NTS) {
-    sm.E[r] = 1.0;
+    Ec[r] = 1.0;
     const int a5 = r % 5;  // friction pyramid rows (ConvexMpc.cpp:46-58)
     sm.Ap[0][r] = a5 < 4 ? 1.0 : 0.0;
     sm.Ap[1][r] = a5 < 4 ? ((a5 & 1) ? -mu : mu) : 1.0;
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
         for (int jj = 0; jj < BPT; ++jj) {
           const int j = jb + jj;
           if (j < N) {
-            const double* dj = sm.D + ND * j;
+            const double* dj = Dc + ND * j;
 #pragma unroll
             for (int b = 0; b < 12; ++b) m6[b % 6] = fmax(m6[b % 6], dj[b] * dabs(hc[12 * jj + b]));
           }
@@ -160,8 +163,8 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
         mx1 = fmax(fmax(m6[1], m6[3]), m6[5]);
       } else {
         gen_col<N, BPT, false>(sm, p, A, dtm, j0, jb, [&](int, int b, int ri, double hv) __attribute__((always_inline)) {
-          if (b & 1) mx1 = fmax(mx1, sm.D[ri] * dabs(hv));
-          else mx0 = fmax(mx0, sm.D[ri] * dabs(hv));
+          if (b & 1) mx1 = fmax(mx1, Dc[ri] * dabs(hv));
+          else mx0 = fmax(mx0, Dc[ri] * dabs(hv));
         });
       }
     }
@@ -218,7 +221,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   };
   auto acol = [&](int j) __attribute__((always_inline)) {
     const int f = j / 3, aa = j % 3;
-    const double* e = sm.E + 5 * f;
+    const double* e = Ec + 5 * f;
     const double* a0 = sm.Ap[0] + 5 * f;
     const double* a1 = sm.Ap[1] + 5 * f;
     double mx;
@@ -227,12 +230,12 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     else
       mx = dmax(dmax(dmax(dmax(dabs(a1[0]) * e[0], dabs(a1[1]) * e[1]), dabs(a1[2]) * e[2]), dabs(a1[3]) * e[3]),
                 e[4] * dabs(a1[4]));
-    return mx * sm.D[j];
+    return mx * Dc[j];
   };
   auto arow = [&](int r) __attribute__((always_inline)) {
     const int f = r / 5, k5 = r % 5;
-    const double e = sm.E[r];
-    const double* d = sm.D + 3 * f;
+    const double e = Ec[r];
+    const double* d = Dc + 3 * f;
     if (k5 == 4) return (e * dabs(sm.Ap[1][r])) * d[2];
     return dmax((e * dabs(sm.Ap[0][r])) * d[k5 >> 1], (dabs(sm.Ap[1][r]) * e) * d[2]);
   };
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     // new scaling factors from the current D, E (every thread reads before anyone writes)
     double dtv = 1.0;
     if (lead && j0 < n) {
-      const double pc = (c_s * sm.D[j0]) * cm;
+      const double pc = (c_s * Dc[j0]) * cm;
       dtv = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j0))));
     }
     double et[SC::RPT];
@@ -274,21 +277,24 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
       const int r = t + NTS * rr;
       et[rr] = r < m ? 1.0 / sqrt(limit_scaling(arow(r))) : 1.0;
     }
-    __syncthreads();
+    double* const Dn = sm.D[(pass + 1) & 1];
+    double* const En = sm.E[(pass + 1) & 1];
 #pragma unroll
     for (int rr = 0; rr < SC::RPT; ++rr) {
       const int r = t + NTS * rr;
-      if (r < m) sm.E[r] *= et[rr];
+      if (r < m) En[r] = Ec[r] * et[rr];
     }
     if (lead && j0 < n) {
       sm.q[j0] = dtv * sm.q[j0];
-      sm.D[j0] = sm.D[j0] * dtv;
+      Dn[j0] = Dc[j0] * dtv;
     }
     __syncthreads();
+    Dc = Dn;
+    Ec = En;
     cm = colmax(false);  // column norms of the D-scaled P (cost normalization)
     double sv = 0.0, qv = 0.0;
     if (lead && j0 < n) {
-      sv = (c_s * sm.D[j0]) * cm;
+      sv = (c_s * Dc[j0]) * cm;
       qv = dabs(sm.q[j0]);
     }
     block_sum_max<SC::NWS>(sv, qv, sm.red);
@@ -302,16 +308,14 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   }
   __syncthreads();
   double* out = img + (size_t)inst * SI::SIZE;
+  // (the A entries the passes used are not handed over: wave_kernel derives them from mu or the
+  // warm slot as above; this tick's raw gradient only matters to osqp_update_P, i.e. warm slots)
   if (lead && j0 < n) {
-    out[SI::D + j0] = sm.D[j0];
+    out[SI::D + j0] = Dc[j0];
     out[SI::Q + j0] = sm.q[j0];
-    out[SI::QN + j0] = sm.qn[j0];
+    if (ws) out[SI::QN + j0] = sm.qn[j0];
   }
-  for (int r = t; r < m; r += NTS) {
-    out[SI::E + r] = sm.E[r];
-    out[SI::AP + r] = sm.Ap[0][r];
-    out[SI::AP + m + r] = sm.Ap[1][r];
-  }
+  for (int r = t; r < m; r += NTS) out[SI::E + r] = Ec[r];
   if (t == 0) {
     out[SI::CS] = c_s;
     out[SI::MODE] = (double)mode;
@@ -447,23 +451,34 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 
   WV_MARK(3);
 
-  // ---- 3. OSQP scale_data: the image scale_kernel wrote (D, E, q~, raw q, A entries, c, branch) ----
+  // ---- 3. OSQP scale_data: the image scale_kernel wrote (D, E, q~, c, branch; raw q if warm) ------
   using SI = ScaleImg<N>;
   const double* im = img + (size_t)inst * SI::SIZE;
+  const double c_s = im[SI::CS];
+  const int mode = (int)im[SI::MODE];  // 0 cold, 1 osqp_update_P, 2 OsqpEigen re-init
   for (int j = t; j < n; j += NT) {
     HS.D[j] = im[SI::D + j];
     HS.q[j] = im[SI::Q + j];
-    HS.qn[j] = im[SI::QN + j];
+    if (mode == 1) HS.qn[j] = im[SI::QN + j];
   }
-  for (int r = t; r < m; r += NT) {
-    HS.E[r] = im[SI::E + r];
-    HS.Ap[0][r] = im[SI::AP + r];
-    HS.Ap[1][r] = im[SI::AP + m + r];
-  }
-  const double c_s = im[SI::CS];
-  const int mode = (int)im[SI::MODE];  // 0 cold, 1 osqp_update_P, 2 OsqpEigen re-init
+  for (int r = t; r < m; r += NT) HS.E[r] = im[SI::E + r];
   // Warm start (A1RobotControl.h:67 member solver, :522-538): the slot of the previous tick.
   double* const ws = wstate ? wstate + (size_t)inst * WL::SIZE : nullptr;
+  // The unscaled constraint entries of row ri (ConvexMpc.cpp:46-58), as scale_kernel used them:
+  // [0] on fx (rows 0, 1) / fy (rows 2, 3), [1] on fz.  Set once per solver init (friction pyramid
+  // of this tick's mu); osqp_update_P keeps the previous A: unscale_data of the previous A~ with the
+  // previous scaling (the same expressions as scale_kernel's, so the same bits).
+  auto ap_of = [&](int ri, int which) __attribute__((always_inline)) -> double {
+    const int f = ri / 5, k5 = ri % 5;
+    if (mode == 1) {
+      const double ei = 1. / ws[WL::E + ri];
+      if (which == 0) return k5 < 4 ? (ws[WL::AK + ri] * ei) * (1. / ws[WL::D + 3 * f + (k5 >> 1)]) : 0.0;
+      return (ws[WL::AK + m + ri] * ei) * (1. / ws[WL::D + 3 * f + 2]);
+    }
+    const double mu = rec[MPCQP_REC_MU];
+    if (which == 0) return k5 < 4 ? 1.0 : 0.0;
+    return k5 < 4 ? ((k5 & 1) ? -mu : mu) : 1.0;
+  };
   wave_sync();
   const double cost_c = c_s, cinv = 1. / c_s;
   WV_MARK(4);
@@ -493,9 +508,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     Ev[r] = kv ? HS.E[ri] : 1.0;
     E4[r] = kv ? HS.E[r4] : 1.0;
     // A~ = E A D: row a < 4 has A on fx (a < 2) / fy (a >= 2) and on fz; row 4 on fz
-    AK0[r] = kv ? (HS.Ap[0][ri] * Ev[r]) * HS.D[cf + (a >> 1)] : 0.0;
-    AK1[r] = kv ? (HS.Ap[1][ri] * Ev[r]) * HS.D[cf + 2] : 0.0;
-    AK4[r] = kv ? (HS.Ap[1][r4] * E4[r]) * HS.D[cf + 2] : 0.0;
+    AK0[r] = kv ? (ap_of(ri, 0) * Ev[r]) * HS.D[cf + (a >> 1)] : 0.0;
+    AK1[r] = kv ? (ap_of(ri, 1) * Ev[r]) * HS.D[cf + 2] : 0.0;
+    AK4[r] = kv ? (ap_of(r4, 1) * E4[r]) * HS.D[cf + 2] : 0.0;
     // bounds (ConvexMpc.cpp:223-245), clipped to +-OSQP_INFTY, scaled by E
     double l4 = fzmin * cont, u4 = fzmax * cont;
     l4 = dmin(dmax(l4, -OSQP_INF), OSQP_INF);

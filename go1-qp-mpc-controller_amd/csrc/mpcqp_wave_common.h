@@ -57,7 +57,6 @@ struct WSmem {
       double D[C::n], Dt[C::n], q[C::n], E[C::m];
       double lam[N][ND];  // gradient adjoint lambda_k (states 0..11)
       double vec[2][16];  // sequential 13-vectors (gradient forward sweep)
-      double Ap[2][C::m];  // unscaled A entries per row: [0] on fx / fy (rows 0-3), [1] on fz
       double qn[C::n];     // this tick's gradient (warm start: q of the Ruiz passes is the old one)
     } h;
     struct Fs {  // solve: per-step factors (the factorization itself runs in registers)
@@ -528,15 +527,14 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
 // Ruiz equilibration is embarrassingly parallel over the columns of P~ = c D H D, so it runs before
 // wave_kernel with one thread per column (NTS threads per robot) and, for n <= 128, the column of H
 // generated once into registers instead of once per pass.  It writes a per-robot image (ScaleImg:
-// D, E, the scaled gradient q~, the raw gradient, the A entries the passes used, c, the warm-start
-// branch) that wave_kernel reads in place of its own setup.  H's columns come from the same closed
+// D, E, the scaled gradient q~, c, the warm-start branch, and for warm slots the raw gradient) that
+// wave_kernel reads in place of its own setup.  H's columns come from the same closed
 // form as before (see gen_col), so every norm is binary64; only the order of the cost-scaling sum
 // over columns differs from the single-wave version (a different but equally exact summation).
 template <int N>
 struct ScaleImg {
   static constexpr int n = ND * N, m = CD * N;
-  static constexpr int D = 0, E = D + n, Q = E + m, QN = Q + n, AP = QN + n, CS = AP + 2 * m, MODE = CS + 1,
-                       SIZE = MODE + 1;
+  static constexpr int D = 0, E = D + n, Q = E + m, QN = Q + n, CS = QN + n, MODE = CS + 1, SIZE = MODE + 1;
   static_assert(SIZE == scale_image_doubles(N), "scale image layout");
 };
 
@@ -564,7 +562,7 @@ struct ScaleSmem {
   using C = Cfg<N>;
   alignas(16) double Bw[N][3][ND];
   double rec[C::REC];
-  double D[C::n], q[C::n], qn[C::n], E[C::m];
+  double D[2][C::n], q[C::n], qn[C::n], E[2][C::m];  // D, E double-buffered over the Ruiz passes
   double lam[N][ND];
   double vec[2][16];
   double Ap[2][C::m];
