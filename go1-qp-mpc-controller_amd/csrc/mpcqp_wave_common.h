@@ -545,7 +545,10 @@ struct ScaleCfg {
 #define MPCQP_SCALE_TPC 2
 #endif
   static constexpr bool HREG = N <= 10;              // the thread's entries cached in registers
-  static constexpr int TPC = HREG ? MPCQP_SCALE_TPC : 1;  // threads per column (adjacent lanes)
+#ifndef MPCQP_SCALE_TPC_LONG
+#define MPCQP_SCALE_TPC_LONG 1
+#endif
+  static constexpr int TPC = HREG ? MPCQP_SCALE_TPC : MPCQP_SCALE_TPC_LONG;  // threads per column (adjacent lanes)
   static constexpr int BPT = (N + TPC - 1) / TPC;    // horizon blocks of the column per thread
   static constexpr int NTS = ((TPC * n + 63) / 64) * 64;
   static constexpr int NWS = NTS / 64;
