@@ -507,10 +507,41 @@ __device__ __forceinline__ void schur_solve(SchurLds<N>& F, const double (&W)[R]
 // update_info mat_vec (osqp auxil.c; oracle/mpc_oracle.c:760) instead of being carried through the
 // iterations: z = B6 (D v) on the impulse lanes, M z, then B6' (M z) + R D v on the variable lanes.
 // DVv[r] = D v and Dd[r] = D in the variable layout.  Uses wv / qv (not Q or B).
+// M z without an LDS round trip: z's four row copies (rowbcast4) feed row_newbcast FMAs, so lane
+// (k, c) accumulates, step l ascending, s2[f] += alpha_kl z_(l,f) and s1[f] += beta_kl z_(l,f) for
+// all six components f and keeps s1[c]: the same fma chains as summing z_(l,c) read from LDS.
+// alpha_kl and beta_kl are exact integers formed in binary64 (no integer division).
+#define PX_F(A, C, L) "v_fmac_f64_dpp %[" A "], %[x], %[" C "] row_newbcast:%[" L "] row_mask:0xf bank_mask:0xf\n\t"
+// s2[f] += bcast_(L0+f)(x) * al, s1[f] += bcast_(L0+f)(x) * be, f < 6 (lanes L0 .. L0+5 of x's row)
+template <int L0>
+__device__ __forceinline__ void px_step(double x, double al, double be, double (&s1)[6], double (&s2)[6]) {
+  static_assert(L0 + 5 <= 15, "a step's six unknowns inside one DPP row");
+  asm("s_nop 4\n\t"
+      PX_F("b0", "al", "l0") PX_F("b1", "al", "l1") PX_F("b2", "al", "l2") PX_F("b3", "al", "l3")
+      PX_F("b4", "al", "l4") PX_F("b5", "al", "l5")
+      PX_F("a0", "be", "l0") PX_F("a1", "be", "l1") PX_F("a2", "be", "l2") PX_F("a3", "be", "l3")
+      PX_F("a4", "be", "l4") PX_F("a5", "be", "l5")
+      : [a0] "+v"(s1[0]), [a1] "+v"(s1[1]), [a2] "+v"(s1[2]), [a3] "+v"(s1[3]), [a4] "+v"(s1[4]), [a5] "+v"(s1[5]),
+        [b0] "+v"(s2[0]), [b1] "+v"(s2[1]), [b2] "+v"(s2[2]), [b3] "+v"(s2[3]), [b4] "+v"(s2[4]), [b5] "+v"(s2[5])
+      : [x] "v"(x), [al] "v"(al), [be] "v"(be), [l0] "n"(L0), [l1] "n"(L0 + 1), [l2] "n"(L0 + 2),
+        [l3] "n"(L0 + 3), [l4] "n"(L0 + 4), [l5] "n"(L0 + 5));
+}
+#undef PX_F
+// one component of a step whose unknowns straddle two DPP rows
+template <int L>
+__device__ __forceinline__ void px_one(double x, double al, double be, double& s1, double& s2) {
+  asm("s_nop 4\n\t"
+      "v_fmac_f64_dpp %[b], %[x], %[al] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[a], %[x], %[be] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"
+      : [a] "+v"(s1), [b] "+v"(s2)
+      : [x] "v"(x), [al] "v"(al), [be] "v"(be), [l] "n"(L));
+}
+// q2c = 2 q_(6+c) of the lane's impulse component c, r2i = 2 r_idx of its variable component (per-lane
+// constants the kernel loads once: a per-lane index into the parameters is a memory round trip)
 template <int N, int R, class SM>
 __device__ __forceinline__ void schur_px(const SM& sm, SchurLds<N>& F, const mpcqp_params& p, const Adisc& A,
-                                         double dtm, double cost_c, const double (&DVv)[R], const double (&Dd)[R],
-                                         const bool (&vvr)[R], double (&out)[R]) {
+                                         double dtm, double cost_c, double q2c, double r2i, const double (&DVv)[R],
+                                         const double (&Dd)[R], const bool (&vvr)[R], double (&out)[R]) {
   constexpr int NI = SchurCfg<N>::NI;
   const int t = threadIdx.x, q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
   const bool av = a < 3;
@@ -522,6 +553,7 @@ __device__ __forceinline__ void schur_px(const SM& sm, SchurLds<N>& F, const mpc
   wave_sync();
   // impulse role, lane i = 6 k + c: z = B6_k (D v)_k (rows 0-2: B_w, rows 3-5: dt/m leg sums)
   const int i = t < NI ? t : NI - 1, k = i / 6, c = i % 6;
+  double z;
   {
     const double* w = &F.wv[12 * k];
     const double* bw = sm.Bw[k][c < 3 ? c : 0];
@@ -530,32 +562,46 @@ __device__ __forceinline__ void schur_px(const SM& sm, SchurLds<N>& F, const mpc
     for (int j = 0; j < 12; ++j) zw += bw[j] * w[j];
     const int cc = c < 3 ? 0 : c - 3;
     const double zv = dtm * (((w[cc] + w[3 + cc]) + w[6 + cc]) + w[9 + cc]);
-    F.qv[t] = t < NI ? (c < 3 ? zw : zv) : 0.0;
+    z = t < NI ? (c < 3 ? zw : zv) : 0.0;
   }
-  wave_sync();
   // (M z)_(k,c) = Qv_c sum_l beta_kl z_(l,c) + (Ac6' Qp Ac6 sum_l alpha_kl z_l)_c
   double mz;
   {
-    double s1 = 0.0, s2[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int l = 0; l < N; ++l) {
-      const double* zl = &F.qv[6 * l];
-      const double al = alpha_jl(N, k, l), be = (double)(N - (k > l ? k : l));
-      s1 += be * zl[c];
-#pragma unroll
-      for (int f = 0; f < 6; ++f) s2[f] += al * zl[f];
-    }
+    double zc[4];
+    rowbcast4(z, zc[0], zc[1], zc[2], zc[3]);
+    double s1[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, s2[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    // alpha_kl = sum_{i >= max(k,l)} (i-k)(i-l): l >= k: (l-k) T1(N-1-l) + T2(N-1-l); l < k:
+    // (k-l) T1(N-1-k) + T2(N-1-k), T1(m) = m(m+1)/2, T2(m) = m(m+1)(2m+1)/6 (all exact integers)
+    const double mk = (double)(N - 1 - k);
+    const double t1k = mk * (mk + 1.0) * 0.5;
+    const double t2k = (mk * (mk + 1.0) * (2.0 * mk + 1.0)) / 6.0;
+    sfor<0, N>([&](auto LL) __attribute__((always_inline)) {
+      constexpr int l = decltype(LL)::value, L0 = 6 * l;
+      constexpr int ml = N - 1 - l;
+      constexpr double t1l = ml * (ml + 1) / 2, t2l = ml * (ml + 1) * (2 * ml + 1) / 6;
+      const double al = k <= l ? fma((double)(l - k), t1l, t2l) : fma((double)(k - l), t1k, t2k);
+      const double be = (double)(N - (k > l ? k : l));
+      if constexpr ((L0 >> 4) == ((L0 + 5) >> 4)) {
+        px_step<L0 & 15>(zc[L0 >> 4], al, be, s1, s2);
+      } else {
+        sfor<0, 6>([&](auto FF) __attribute__((always_inline)) {
+          constexpr int f = decltype(FF)::value, Lf = L0 + f;
+          px_one<Lf & 15>(zc[Lf >> 4], al, be, s1[f], s2[f]);
+        });
+      }
+    });
     // w_e = 2 q_e (Ac6 s2)_e; Ac6 = A[0:6, 6:12]
     const double w0 = (2.0 * p.q_weights[0]) * (A.ad0 * s2[0] + A.ad1 * s2[1]);
     const double w1 = (2.0 * p.q_weights[1]) * ((-A.ad1) * s2[0] + A.ad0 * s2[1]);
-    double wc = 0.0;
+    double wc = 0.0, s1c = s1[0];
 #pragma unroll
     for (int e = 2; e < 6; ++e) wc = c == e ? (2.0 * p.q_weights[e]) * (A.dt * s2[e]) : wc;
+#pragma unroll
+    for (int e = 1; e < 6; ++e) s1c = c == e ? s1[e] : s1c;
     // (Ac6' w)_c: c = 0, 1 mix the yaw rotation; c = 2: dt w_2; c >= 3: dt w_c
     const double ac = c == 0 ? A.ad0 * w0 + (-A.ad1) * w1 : (c == 1 ? A.ad1 * w0 + A.ad0 * w1 : A.dt * wc);
-    mz = (2.0 * p.q_weights[6 + c]) * s1 + ac;
+    mz = q2c * s1c + ac;
   }
-  wave_sync();
   if (t < NI) F.qv[t] = mz;
   wave_sync();
   // variable role: (B6' M z)_j + 2 r_j (D v)_j, times c D
@@ -566,7 +612,7 @@ __device__ __forceinline__ void schur_px(const SM& sm, SchurLds<N>& F, const mpc
     const double* mk = &F.qv[6 * kc];
     const double hv = ((((sm.Bw[kc][0][idx] * mk[0] + sm.Bw[kc][1][idx] * mk[1]) + sm.Bw[kc][2][idx] * mk[2]) +
                         dtm * mk[3 + (av ? a : 2)]) +
-                       (2.0 * p.r_weights[idx]) * DVv[r]);
+                       r2i * DVv[r]);
     out[r] = vvr[r] ? (cost_c * Dd[r]) * hv : 0.0;
   }
   wave_sync();

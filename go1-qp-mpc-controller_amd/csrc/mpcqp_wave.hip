@@ -605,20 +605,31 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       PX[r] = vvr[r] ? (c_s * Dv[r]) * hv : 0.0;
     }
   }
-  // D and E of the lane's variable / rows, reloaded from the image (volatile: never hoisted into
-  // loop-carried registers)
-  // (a global-address-space pointer: global_load, not flat_load, whose lgkmcnt share would also
-  // wait on the LDS traffic in flight)
-  using gvd = const volatile __attribute__((address_space(1))) double;
-  gvd* imv = (gvd*)im;
+  // D and E of the lane's variable / rows, reloaded from the image where they are needed (the
+  // factorizations, the checks, the epilogue) instead of being held in loop-carried registers: the
+  // element offset goes through an opaque copy, so the loads are neither hoisted out of the loop
+  // nor merged across uses.  Plain loads, not volatile ones (each volatile load was followed by its
+  // own wait for the memory round trip); unconditional, at a clamped step, the padding value
+  // selected after (a load under the lane mask became a branch with its own wait).  A
+  // global-address-space pointer: global_load, not flat_load, whose lgkmcnt share would also wait
+  // on the LDS traffic in flight.
+  using gd = const __attribute__((address_space(1))) double;
+  gd* const imv = (gd*)im;
+  auto img_at = [&](int e) __attribute__((always_inline)) -> double {
+    asm volatile("" : "+v"(e));
+    return imv[e];
+  };
   auto dv_of = [&](int r) __attribute__((always_inline)) {
-    return vvr[r] ? imv[SI::D + ND * (4 * r + ig) + idx] : 1.0;
+    const double v = img_at(SI::D + ND * min(4 * r + ig, N - 1) + idx);
+    return vvr[r] ? v : 1.0;
   };
   auto ev_of = [&](int r) __attribute__((always_inline)) {
-    return kvr[r] ? imv[SI::E + CD * (4 * r + ig) + 5 * leg + a] : 1.0;
+    const double v = img_at(SI::E + CD * min(4 * r + ig, N - 1) + 5 * leg + a);
+    return kvr[r] ? v : 1.0;
   };
   auto e4_of = [&](int r) __attribute__((always_inline)) {
-    return kvr[r] ? imv[SI::E + CD * (4 * r + ig) + 5 * leg + 4] : 1.0;
+    const double v = img_at(SI::E + CD * min(4 * r + ig, N - 1) + 5 * leg + 4);
+    return kvr[r] ? v : 1.0;
   };
   // rows 0-3: l = 0 / u = +inf (rows 0, 2) or l = -inf / u = 0 (rows 1, 3): always inequalities
   auto lo03 = [&](double ev) __attribute__((always_inline)) { return (a & 1) ? ev * -OSQP_INF : ev * 0.0; };
@@ -630,6 +641,11 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 
   // ---- 5. ADMM (osqp_solve) ------------------------------------------------------------------------
   auto& F = sm.u.f;
+  // per-lane weights, loaded once (a per-lane index into the kernel parameters is a memory round
+  // trip): 2 r of the lane's variable component, 2 q_(6+c) of its impulse component (KS = 1)
+  double R2I = 2.0 * p.r_weights[idx], Q2C = 2.0 * p.q_weights[6 + (t < 6 * N ? t : 0) % 6];
+  keep(R2I);
+  keep(Q2C);
   // KS = 1: the lane's rows of R'^-1 (mpcqp_schur.h), set per rho
   double SRI[KS == 1 ? R : 1][3];
   (void)SRI;
@@ -639,10 +655,14 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       double dd[R], dvv[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
+#ifdef MPCQP_XPXREG
+        dd[r] = DI[r];
+#else
         dd[r] = dv_of(r);
+#endif
         dvv[r] = dd[r] * v[r];
       }
-      schur_px<N, R>(sm, F, p, A, dtm, cost_c, dvv, dd, vvr, out);
+      schur_px<N, R>(sm, F, p, A, dtm, cost_c, Q2C, R2I, dvv, dd, vvr, out);
     }
   };
   double rho = rho0, rinv = 1. / rho0, pri_res = 0.0, dua_res = 0.0;
@@ -681,7 +701,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
 #pragma unroll
           for (int row = 0; row < 5; ++row) s += (coef(row, av ? a : 2) * (row == 4 ? r4 : rho)) * coef(row, b);
           const double db = b == 0 ? d0 : (b == 1 ? d1 : d2);
-          const double rt = (av && a == b ? cost_c * (2.0 * p.r_weights[idx]) : 0.0) +
+          const double rt = (av && a == b ? cost_c * R2I : 0.0) +
                             ((1.0 / da) * ((av && a == b ? sigma : 0.0) + s)) * (1.0 / db);
           if (kvr[r] && av && b >= a) {
             if constexpr (KS == 0) F.Rt[k][leg][sym6(a, b)] = rt;
@@ -946,136 +966,129 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     else update(IC<0>{});
 
     if (tm_it) WV_MARK(46);
+    const bool tm_ck = iter == 75;  // (a termination check + adapt_rho iteration, timed)
+    if (tm_ck) WV_MARK(48);
     if (need_info) {
       // ---- update_info / check_termination / adapt_rho (osqp.c, auxil.c) ----
       if constexpr (KS == 1) px_of(X, PX);
-      double mx[14];
+      if (tm_ck) WV_MARK(50);
+      // The norms of update_info / check_termination / compute_rho_estimate, and the first-level
+      // quantities of both infeasibility tests (||E dy||, the support term of dy, ||D dx||, q'dx:
+      // needed at nearly every check, since dua_res is rarely small before convergence), reduced
+      // in one batch of independent wave reductions.  Norms that enter only as max(a, b) share a
+      // slot (a max is exact in any grouping): [0] |E^-1 (A~x - z)|, [1] |A~x - z|,
+      // [2] max(|E^-1 z|, |E^-1 A~x|), [3] max(|z|, |A~x|), [4] |D^-1 dual|, [5] |dual|,
+      // [6] max(|D^-1 q~|, |D^-1 A~'y|, |D^-1 P~x|), [7] max(|q~|, |A~'y|, |P~x|).
+      constexpr int NM = 8;
+      double mx[NM];
 #pragma unroll
-      for (int k = 0; k < 14; ++k) mx[k] = 0.0;
+      for (int k = 0; k < NM; ++k) mx[k] = 0.0;
+      double nd = 0.0, lh = 0.0, nx = 0.0, qd = 0.0, dyp[R], dyp4[R];
+      auto proj = [&](double d, double lo, double hi) __attribute__((always_inline)) {
+        // delta_y projected onto the polar of the recession cone of [l, u]
+        if (hi > OSQP_INF * MIN_SCALING) {
+          if (lo < -OSQP_INF * MIN_SCALING) d = 0.0;
+          else d = dmin(d, 0.0);
+        } else if (lo < -OSQP_INF * MIN_SCALING) {
+          d = dmax(d, 0.0);
+        }
+        return d;
+      };
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const double xp = dpp<QP_PRIM>(X[r]), xz = dpp<QP_B2>(X[r]);
         const double ax = AK0[r] * xp + AK1[r] * xz, ax4 = AK4[r] * xz;
         const double aty = quad_at(Y[r], Y4[r], AK0[r], AK1[r], AK4[r], a);
+        const double evr = ev_of(r), e4r = e4_of(r);
         if (kvr[r]) {
-          const double ei = recip(ev_of(r)), ei4 = recip(e4_of(r));
+          const double ei = recip(evr), ei4 = recip(e4r);
           const double pr = ax + (-1.0) * Z[r], pr4 = ax4 + (-1.0) * Z4[r];
           mx[0] = nmax(mx[0], nmax(dabs(ei * pr), dabs(ei4 * pr4)));
           mx[1] = nmax(mx[1], nmax(dabs(pr), dabs(pr4)));
-          mx[2] = nmax(mx[2], nmax(dabs(ei * Z[r]), dabs(ei4 * Z4[r])));
-          mx[3] = nmax(mx[3], nmax(dabs(Z[r]), dabs(Z4[r])));
-          mx[4] = nmax(mx[4], nmax(dabs(ei * ax), dabs(ei4 * ax4)));
-          mx[5] = nmax(mx[5], nmax(dabs(ax), dabs(ax4)));
+          mx[2] = nmax(mx[2], nmax(nmax(dabs(ei * Z[r]), dabs(ei4 * Z4[r])), nmax(dabs(ei * ax), dabs(ei4 * ax4))));
+          mx[3] = nmax(mx[3], nmax(nmax(dabs(Z[r]), dabs(Z4[r])), nmax(dabs(ax), dabs(ax4))));
         }
         if (vvr[r]) {
           const double d = (Qv[r] + 1.0 * PX[r]) + 1.0 * aty;
-          mx[6] = nmax(mx[6], dabs(DI[r] * d));
-          mx[7] = nmax(mx[7], dabs(d));
-          mx[8] = nmax(mx[8], dabs(DI[r] * Qv[r]));
-          mx[9] = nmax(mx[9], dabs(Qv[r]));
-          mx[10] = nmax(mx[10], dabs(DI[r] * aty));
-          mx[11] = nmax(mx[11], dabs(aty));
-          mx[12] = nmax(mx[12], dabs(DI[r] * PX[r]));
-          mx[13] = nmax(mx[13], dabs(PX[r]));
+          mx[4] = nmax(mx[4], dabs(DI[r] * d));
+          mx[5] = nmax(mx[5], dabs(d));
+          mx[6] = nmax(mx[6], nmax(nmax(dabs(DI[r] * Qv[r]), dabs(DI[r] * aty)), dabs(DI[r] * PX[r])));
+          mx[7] = nmax(mx[7], nmax(nmax(dabs(Qv[r]), dabs(aty)), dabs(PX[r])));
+        }
+        // is_primal_infeasible: ||E dy||_inf and u'max(dy, 0) + l'min(dy, 0) of the projected dy
+        const double lo = lo03(evr), hi = hi03(evr);
+        const double d = proj(DY[r], lo, hi), d4 = proj(DY4[r], L4[r], U4[r]);
+        dyp[r] = d;
+        dyp4[r] = d4;
+        if (kvr[r]) {
+          nd = nmax(nd, nmax(dabs(evr * d), dabs(e4r * d4)));
+          lh += hi * dmax(d, 0.0) + lo * dmin(d, 0.0);
+          if (a == 0) lh += U4[r] * dmax(d4, 0.0) + L4[r] * dmin(d4, 0.0);
+        }
+        // is_dual_infeasible: ||D dx||_inf and q~'dx
+        if (vvr[r]) {
+          nx = nmax(nx, dabs(dv_of(r) * DX[r]));
+          qd += Qv[r] * DX[r];
         }
       }
 #pragma unroll
-      for (int k = 0; k < 14; ++k) mx[k] = wave_nmax(mx[k]);
+      for (int k = 0; k < NM; ++k) mx[k] = wave_nmax(mx[k]);
+      const double ndy = wave_nmax(nd), ndx = wave_nmax(nx);
+      lh = wave_sum(lh);
+      qd = wave_sum(qd);
       pri_res = mx[0];
-      dua_res = cinv * mx[6];
+      dua_res = cinv * mx[4];
       iters = iter;
+      if (tm_ck) WV_MARK(51);
       auto check = [&](bool approx) __attribute__((always_inline)) -> int {
         double eps_abs = p.eps_abs, eps_rel = p.eps_rel, eps_pinf = p.eps_prim_inf, eps_dinf = p.eps_dual_inf;
         if (pri_res > OSQP_INF || dua_res > OSQP_INF) return MPCQP_STATUS_NON_CVX;
         if (approx) { eps_abs *= 10; eps_rel *= 10; eps_pinf *= 10; eps_dinf *= 10; }
-        const double eps_prim = eps_abs + eps_rel * dmax(mx[2], mx[4]);
+        const double eps_prim = eps_abs + eps_rel * mx[2];
         const bool prim_ok = pri_res < eps_prim;
         bool prim_inf = false, dual_inf = false;
-        if (!prim_ok) {
-          // is_primal_infeasible: delta_y projected onto the polar of the recession cone
-          double nd = 0.0, lh = 0.0, dyp[R], dyp4[R];
+        if (!prim_ok && ndy > DIV_TOL && lh < eps_pinf * ndy) {
+          double an = 0.0;
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            auto proj = [&](double d, double lo, double hi) __attribute__((always_inline)) {
-              if (hi > OSQP_INF * MIN_SCALING) {
-                if (lo < -OSQP_INF * MIN_SCALING) d = 0.0;
-                else d = dmin(d, 0.0);
-              } else if (lo < -OSQP_INF * MIN_SCALING) {
-                d = dmax(d, 0.0);
-              }
-              return d;
-            };
-            const double evr = ev_of(r), e4r = e4_of(r);
-            const double lo = lo03(evr), hi = hi03(evr);
-            const double d = proj(DY[r], lo, hi), d4 = proj(DY4[r], L4[r], U4[r]);
-            dyp[r] = d;
-            dyp4[r] = d4;
-            if (kvr[r]) {
-              nd = nmax(nd, nmax(dabs(evr * d), dabs(e4r * d4)));
-              lh += hi * dmax(d, 0.0) + lo * dmin(d, 0.0);
-              if (a == 0) lh += U4[r] * dmax(d4, 0.0) + L4[r] * dmin(d4, 0.0);
-            }
+            const double atd = quad_at(dyp[r], dyp4[r], AK0[r], AK1[r], AK4[r], a);
+            if (vvr[r]) an = nmax(an, dabs(DI[r] * atd));
           }
-          const double ndy = wave_nmax(nd);
-          if (ndy > DIV_TOL) {
-            lh = wave_sum(lh);
-            if (lh < eps_pinf * ndy) {
-              double an = 0.0;
-#pragma unroll
-              for (int r = 0; r < R; ++r) {
-                const double atd = quad_at(dyp[r], dyp4[r], AK0[r], AK1[r], AK4[r], a);
-                if (vvr[r]) an = nmax(an, dabs(DI[r] * atd));
-              }
-              an = wave_nmax(an);
-              prim_inf = an < eps_pinf * ndy;
-            }
-          }
+          an = wave_nmax(an);
+          prim_inf = an < eps_pinf * ndy;
         }
-        const double eps_dual = eps_abs + eps_rel * (cinv * dmax(dmax(mx[8], mx[10]), mx[12]));
+        const double eps_dual = eps_abs + eps_rel * (cinv * mx[6]);
         const bool dual_ok = dua_res < eps_dual;
-        if (!dual_ok) {
+        if (!dual_ok && ndx > DIV_TOL && qd < cost_c * eps_dinf * ndx) {
           // is_dual_infeasible (P~ delta_x = P~x_new - P~x_old)
-          double nx = 0.0, qd = 0.0;
+          double pd = 0.0, PDX[R];
+          if constexpr (KS == 1) px_of(DX, PDX);
 #pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (vvr[r]) {
-              nx = nmax(nx, dabs(dv_of(r) * DX[r]));
-              qd += Qv[r] * DX[r];
-            }
-          const double ndx = wave_nmax(nx);
-          if (ndx > DIV_TOL) {
-            qd = wave_sum(qd);
-            if (qd < cost_c * eps_dinf * ndx) {
-              double pd = 0.0, PDX[R];
-              if constexpr (KS == 1) px_of(DX, PDX);
+          for (int r = 0; r < R; ++r) {
+            if constexpr (KS == 0) PDX[r] = PX[r] - PXO[r];
+            if (vvr[r]) pd = nmax(pd, dabs(DI[r] * PDX[r]));
+          }
+          pd = wave_nmax(pd);
+          if (pd < cost_c * eps_dinf * ndx) {
+            double viol = 0.0;
 #pragma unroll
-              for (int r = 0; r < R; ++r) {
-                if constexpr (KS == 0) PDX[r] = PX[r] - PXO[r];
-                if (vvr[r]) pd = nmax(pd, dabs(DI[r] * PDX[r]));
-              }
-              pd = wave_nmax(pd);
-              if (pd < cost_c * eps_dinf * ndx) {
-                double viol = 0.0;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                  const double dp = dpp<QP_PRIM>(DX[r]), dz = dpp<QP_B2>(DX[r]);
-                  const double evr = ev_of(r);
-                  const double v = (1.0 / evr) * (AK0[r] * dp + AK1[r] * dz);
-                  const double v4 = (1.0 / e4_of(r)) * (AK4[r] * dz);
-                  const double lo = lo03(evr), hi = hi03(evr);
-                  if (kvr[r]) {
-                    if ((hi < OSQP_INF * MIN_SCALING && v > eps_dinf * ndx) ||
-                        (lo > -OSQP_INF * MIN_SCALING && v < -eps_dinf * ndx))
-                      viol = 1.0;
-                    if ((U4[r] < OSQP_INF * MIN_SCALING && v4 > eps_dinf * ndx) ||
-                        (L4[r] > -OSQP_INF * MIN_SCALING && v4 < -eps_dinf * ndx))
-                      viol = 1.0;
-                  }
-                }
-                viol = wave_nmax(viol);
-                dual_inf = viol == 0.0;
+            for (int r = 0; r < R; ++r) {
+              const double dp = dpp<QP_PRIM>(DX[r]), dz = dpp<QP_B2>(DX[r]);
+              const double evr = ev_of(r);
+              const double v = (1.0 / evr) * (AK0[r] * dp + AK1[r] * dz);
+              const double v4 = (1.0 / e4_of(r)) * (AK4[r] * dz);
+              const double lo = lo03(evr), hi = hi03(evr);
+              if (kvr[r]) {
+                if ((hi < OSQP_INF * MIN_SCALING && v > eps_dinf * ndx) ||
+                    (lo > -OSQP_INF * MIN_SCALING && v < -eps_dinf * ndx))
+                  viol = 1.0;
+                if ((U4[r] < OSQP_INF * MIN_SCALING && v4 > eps_dinf * ndx) ||
+                    (L4[r] > -OSQP_INF * MIN_SCALING && v4 < -eps_dinf * ndx))
+                  viol = 1.0;
               }
             }
+            viol = wave_nmax(viol);
+            dual_inf = viol == 0.0;
           }
         }
         if (prim_ok && dual_ok) return approx ? MPCQP_STATUS_SOLVED_INACCURATE : MPCQP_STATUS_SOLVED;
@@ -1092,8 +1105,8 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
           done = st != MPCQP_STATUS_UNSOLVED;
         }
         if (pass == 1 || done || !is_adapt) continue;
-        const double pr_n = mx[1] / (dmax(mx[3], mx[5]) + DIV_TOL);
-        const double du_n = mx[7] / (dmax(dmax(mx[9], mx[11]), mx[13]) + DIV_TOL);
+        const double pr_n = mx[1] / (mx[3] + DIV_TOL);
+        const double du_n = mx[5] / (mx[7] + DIV_TOL);
         double est = rho * sqrt(pr_n / (du_n + DIV_TOL));
         est = dmin(dmax(est, RHO_MIN), RHO_MAX);
         if (est > rho * p.adaptive_rho_tolerance || est < rho / p.adaptive_rho_tolerance) {
@@ -1102,6 +1115,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
           refactor = !last;
         }
       }
+      if (tm_ck) WV_MARK(52);
       if (last && st == MPCQP_STATUS_UNSOLVED) st = MPCQP_STATUS_MAX_ITER_REACHED;
       if (last) done = true;
       status = st;
@@ -1129,6 +1143,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         }
       }
     }
+    if (tm_ck) WV_MARK(49);
     if (tm_it) WV_MARK(47);
   }
 
@@ -1139,7 +1154,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       ws[WL::RHO] = rho;
       // c and mu reloaded from HBM here rather than carried through the loop (values live across
       // the whole solve are the ones the register allocator parks in AGPRs / scratch)
-      ws[WL::C] = imv[SI::CS];
+      ws[WL::C] = img_at(SI::CS);
       ws[WL::MU] = ((const volatile double*)(recs + (size_t)inst * C::REC))[MPCQP_REC_MU];
     }
 #pragma unroll

@@ -4,7 +4,9 @@
 DEFS=-DMPCQP_PHASE_TIMING`, selected with MPCQP_LIB) and report median shader-clock cycles per
 robot: setup (marks 0 -> 4), each factorization (10 -> 12), the mean ADMM iteration (loop time
 minus factorizations over the iteration count) and, inside iteration 60, the KKT solve (40 -> 45),
-the ADMM update (45 -> 46) and the rest of the iteration (46 -> 47)."""
+the ADMM update (45 -> 46) and the rest of the iteration (46 -> 47); the termination check of
+iteration 75 (48 -> 49: P~x 48 -> 50, norms and reductions 50 -> 51, termination / infeasibility
+tests and adapt_rho 51 -> 52, the rest 52 -> 49)."""
 import argparse
 import json
 import os
@@ -38,7 +40,7 @@ def main():
         torch.cuda.synchronize()
         marks = tr.cpu().numpy().reshape(a.traced, 64, 4)
         res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
-    ph = {k: [] for k in ("setup", "factor", "f_pre", "f_buildS", "f_gj", "f_post", "iter_cycles", "it_kkt",
+    ph = {k: [] for k in ("setup", "factor", "f_pre", "f_buildS", "f_gj", "f_post", "iter_cycles", "check75", "ck_px", "ck_norms", "ck_tests", "ck_tail", "it_kkt",
                           "it_update", "it_rest", "total", "shader_ghz")}
     for b in range(a.traced):
         mk = marks[b]
@@ -62,6 +64,13 @@ def main():
             ph["it_kkt"].append(at[45][0] - at[40][0])
             ph["it_update"].append(at[46][0] - at[45][0])
             ph["it_rest"].append(at[47][0] - at[46][0])
+        if 48 in at and 49 in at:
+            ph["check75"].append(at[49][0] - at[48][0])
+        if all(k in at for k in (48, 50, 51, 52, 49)):
+            ph["ck_px"].append(at[50][0] - at[48][0])
+            ph["ck_norms"].append(at[51][0] - at[50][0])
+            ph["ck_tests"].append(at[52][0] - at[51][0])
+            ph["ck_tail"].append(at[49][0] - at[52][0])
     out = {k: float(np.median(v)) for k, v in ph.items() if v}
     out["mean_iters"] = float(res["iters"][: a.traced].mean())
     out["factorizations_per_robot"] = len(ph["factor"]) / a.traced
