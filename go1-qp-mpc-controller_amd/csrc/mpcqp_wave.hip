@@ -682,8 +682,10 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                      k03 = dpp<QP_B3>(AK0[r]);
         const double k10 = dpp<QP_B0>(AK1[r]), k11 = dpp<QP_B1>(AK1[r]), k12 = dpp<QP_B2>(AK1[r]),
                      k13 = dpp<QP_B3>(AK1[r]);
-        const double dvr = dv_of(r);
-        const double d0 = dpp<QP_B0>(dvr), d1 = dpp<QP_B1>(dvr), d2 = dpp<QP_B2>(dvr);
+        // D^-1 of the foot's three variables from the lanes' own 1 / D (the same correctly rounded
+        // quotients: no reload of D, no division here)
+        const double dir = DI[r];
+        const double i0 = dpp<QP_B0>(dir), i1 = dpp<QP_B1>(dir), i2 = dpp<QP_B2>(dir);
         const double ak4 = AK4[r], r4 = RHO4[r];
         // rows of the foot: r0 [k00,0,k10] r1 [k01,0,k11] r2 [0,k02,k12] r3 [0,k03,k13] r4 [0,0,ak4]
         auto coef = [&](int row, int col) __attribute__((always_inline)) {
@@ -694,15 +696,14 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
           return (col == (row >> 1)) ? kp : 0.0;
         };
         const int k = 4 * r + ig;
-        const double da = a == 0 ? d0 : (a == 1 ? d1 : d2);
+        const double ia = a == 0 ? i0 : (a == 1 ? i1 : i2);
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
           double s = 0.0;
 #pragma unroll
           for (int row = 0; row < 5; ++row) s += (coef(row, av ? a : 2) * (row == 4 ? r4 : rho)) * coef(row, b);
-          const double db = b == 0 ? d0 : (b == 1 ? d1 : d2);
-          const double rt = (av && a == b ? cost_c * R2I : 0.0) +
-                            ((1.0 / da) * ((av && a == b ? sigma : 0.0) + s)) * (1.0 / db);
+          const double ib = b == 0 ? i0 : (b == 1 ? i1 : i2);
+          const double rt = (av && a == b ? cost_c * R2I : 0.0) + (ia * ((av && a == b ? sigma : 0.0) + s)) * ib;
           if (kvr[r] && av && b >= a) {
             if constexpr (KS == 0) F.Rt[k][leg][sym6(a, b)] = rt;
             else F.s.Rt[k][leg][sym6(a, b)] = rt;
