@@ -37,6 +37,22 @@
 namespace mpcqp {
 namespace wv {
 
+// MPCQP_SCALE_TIMING experiment builds: thread 0 of each robot overwrites the first doubles of its
+// own record with {id, s_memtime} pairs (tools/scale_phases.py; the solve that follows is garbage)
+#ifdef MPCQP_SCALE_TIMING
+#define SC_MARK(id)                                                                     \
+  do {                                                                                  \
+    if (threadIdx.x == 0) {                                                             \
+      double* tm_ = const_cast<double*>(recs) + (size_t)blockIdx.x * Cfg<N>::REC + 2 * (id); \
+      tm_[0] = (id);                                                                    \
+      tm_[1] = (double)__builtin_readcyclecounter();                                    \
+    }                                                                                   \
+  } while (0)
+#else
+#define SC_MARK(id) \
+  do {              \
+  } while (0)
+#endif
 template <int N>
 __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kernel(const double* __restrict__ recs, int batch,
                                                                  double* __restrict__ wstate,
@@ -60,6 +76,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     }
     if (__syncthreads_or(bad)) return;  // wave_kernel reports the non-finite record
   }
+  SC_MARK(0);
   const double* rec = sm.rec;
   const double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS], mu = rec[MPCQP_REC_MU];
   Adisc A;
@@ -91,24 +108,37 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     // (sequential over the horizon: wave 0 alone, wave-synchronous; one block barrier at the end)
     if (t < 64) {
       if (t < SD) sm.vec[0][t] = rec[MPCQP_REC_X0 + t];
+      // 2 q of the lane's state, loaded once (indexed by the lane, it is a memory round trip: inside
+      // the sweep it was one per step)
+      double q2t = 2 * p.q_weights[t < ND ? t : 0];
+      keep(q2t);
+      // Branch-free rows of A_d (forward) and A_d' (backward): lane t's row is
+      // fma(c2, v[j2], fma(c1, v[j1], v[t])), the unused terms with a zero coefficient (exact: the
+      // operands are finite).  Per-lane branches serialized the rows, each with its own LDS wait.
+      const int tr = t < SD ? t : 0;
+      const int fj1 = tr <= 1 ? 6 : (tr == 2 ? 8 : (tr <= 5 ? tr + 6 : (tr == 11 ? 12 : tr)));
+      const double fc1 = tr == 0 ? A.ad0 : (tr == 1 ? -A.ad1 : ((tr <= 5 || tr == 11) ? dt : 0.0));
+      const int fj2 = tr <= 1 ? 7 : tr;
+      const double fc2 = tr == 0 ? A.ad1 : (tr == 1 ? A.ad0 : 0.0);
+      const int bj1 = tr == 6 || tr == 7 ? 0 : (tr == 8 ? 2 : (tr >= 9 && tr < ND ? tr - 6 : tr));
+      const double bc1 = tr == 6 ? A.ad0 : (tr == 7 ? A.ad1 : ((tr >= 8 && tr < ND) ? dt : 0.0));
+      const int bj2 = tr == 6 || tr == 7 ? 1 : tr;
+      const double bc2 = tr == 6 ? -A.ad1 : (tr == 7 ? A.ad0 : 0.0);
       wave_sync();
       for (int i = 0; i < N; ++i) {
         if (t < SD) {
           const double* pv = sm.vec[i & 1];
-          double s;
-          if (t == 0) s = (pv[0] + A.ad0 * pv[6]) + A.ad1 * pv[7];
-          else if (t == 1) s = (pv[1] + (-A.ad1) * pv[6]) + A.ad0 * pv[7];
-          else if (t == 2) s = pv[2] + dt * pv[8];
-          else if (t <= 5) s = pv[t] + dt * pv[t + 6];
-          else if (t == 11) s = pv[11] + dt * pv[12];
-          else s = pv[t];
+          const double s = fma(fc2, pv[fj2], fma(fc1, pv[fj1], pv[tr]));
           sm.vec[(i + 1) & 1][t] = s;
-          if (t < ND) sm.lam[i][t] = 2 * p.q_weights[t] * (s - rec[MPCQP_REC_XREF + SD * i + t]);
+          if (t < ND) sm.lam[i][t] = q2t * (s - rec[MPCQP_REC_XREF + SD * i + t]);
         }
         wave_sync();
       }
       for (int j = N - 2; j >= 0; --j) {
-        if (t < ND) sm.lam[j][t] = sm.lam[j][t] + A.atv(t, sm.lam[j + 1]);
+        if (t < ND) {
+          const double* v = sm.lam[j + 1];
+          sm.lam[j][t] = sm.lam[j][t] + fma(bc2, v[bj2], fma(bc1, v[bj1], v[tr]));
+        }
         wave_sync();
       }
     }
@@ -117,6 +147,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   // thread t: column j0 = t / 4, blocks jb .. jb+BPT-1 of it (the column's four threads are a quad)
   constexpr int BPT = SC::BPT;
   const int j0 = t / SC::TPC, jb = (t % SC::TPC) * BPT;
+  SC_MARK(1);
   const bool lead = (t % SC::TPC) == 0;  // the lane that owns the column's per-column values
   // D and E of the current pass (each pass writes the other buffer: no read-before-write barrier)
   double* Dc = sm.D[0];
@@ -244,6 +275,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   // -> osqp_update_P (unscale with the old scaling, rescale with the previous A and q, keep iterates
   // and rho); a changed pattern or mu -> re-init (fresh scaling and rho, the previous unscaled x, y)
   bool pattern_changed = false;
+  SC_MARK(2);
   if (p.scaling > 0 || ws) {
     cm = colmax(true);
     if (ws) pattern_changed = __syncthreads_or(pattern()) != 0;
@@ -264,7 +296,9 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     }
     __syncthreads();
   }
+  SC_MARK(3);
   for (int pass = 0; pass < p.scaling; ++pass) {
+    if (pass == 1) SC_MARK(4);
     // new scaling factors from the current D, E (every thread reads before anyone writes)
     double dtv = 1.0;
     if (lead && j0 < n) {
@@ -307,6 +341,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     c_s *= c_temp;
   }
   __syncthreads();
+  SC_MARK(5);
   double* out = img + (size_t)inst * SI::SIZE;
   // (the A entries the passes used are not handed over: wave_kernel derives them from mu or the
   // warm slot as above; this tick's raw gradient only matters to osqp_update_P, i.e. warm slots)
@@ -320,7 +355,9 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     out[SI::CS] = c_s;
     out[SI::MODE] = (double)mode;
   }
+  SC_MARK(6);
 }
+#undef SC_MARK
 
 // Phase timing (debug builds with -DMPCQP_PHASE_TIMING): lane 0 of each traced robot appends
 // {phase id, s_memtime, s_memrealtime (100 MHz), 0} to the trace buffer instead of check records.
@@ -646,6 +683,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   double R2I = 2.0 * p.r_weights[idx], Q2C = 2.0 * p.q_weights[6 + (t < 6 * N ? t : 0) % 6];
   keep(R2I);
   keep(Q2C);
+  // KS = 0: 2 q_j of the MFMA column j = lane & 15 (factorize_mfma's cQ diagonal)
+  double Q2J = KS == 0 ? 2.0 * p.q_weights[li < ND ? li : 0] : 0.0;
+  keep(Q2J);
   // KS = 1: the lane's rows of R'^-1 (mpcqp_schur.h), set per rho
   double SRI[KS == 1 ? R : 1][3];
   (void)SRI;
@@ -711,7 +751,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
         }
       }
       wave_sync();
-      if constexpr (KS == 0) factorize_mfma<N>(sm, p, A, cost_c, dtm);
+      if constexpr (KS == 0) factorize_mfma<N>(sm, p, A, cost_c, dtm, Q2J);
       else schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI,
                               [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; });
       wave_sync();

@@ -454,7 +454,9 @@ __device__ __forceinline__ void gj_inverse12(mf4& g) {
 
 // The Riccati recursion of c B'Q̄B + R' (R'_k foot blocks in F.Rt) -> G_k^-1, K_k, Acl_k in LDS.
 template <int N, class SM>
-__device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, double c, double dtm) {
+// q2j: 2 q_j of the lane's column j = lane & 15 (j < 12), loaded once by the caller (a per-lane index
+// into the parameters is a memory round trip)
+__device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, double c, double dtm, double q2j) {
   auto& F = sm.u.f;
   const int j = threadIdx.x & 15, grp = threadIdx.x >> 4;
   mf4 Ad, At, cQ, P;
@@ -464,7 +466,7 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
     const bool in = u < 12 && j < 12;
     Ad[v] = in ? A.at(u, j) : 0.0;
     At[v] = in ? A.at(j, u) : 0.0;
-    cQ[v] = (in && u == j) ? c * (2.0 * p.q_weights[u]) : 0.0;
+    cQ[v] = (in && u == j) ? c * q2j : 0.0;
     P[v] = cQ[v];
   }
   for (int k = N - 1; k >= 0; --k) {
