@@ -250,25 +250,28 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     }
     return diff;
   };
+  // A~ column / row norms, branch-free (every operand loaded, the case selected after: per-lane
+  // branches ran the cases one after another, each with its own LDS wait)
   auto acol = [&](int j) __attribute__((always_inline)) {
     const int f = j / 3, aa = j % 3;
     const double* e = Ec + 5 * f;
     const double* a0 = sm.Ap[0] + 5 * f;
     const double* a1 = sm.Ap[1] + 5 * f;
-    double mx;
-    if (aa == 0) mx = dmax(e[0] * dabs(a0[0]), e[1] * dabs(a0[1]));
-    else if (aa == 1) mx = dmax(e[2] * dabs(a0[2]), e[3] * dabs(a0[3]));
-    else
-      mx = dmax(dmax(dmax(dmax(dabs(a1[0]) * e[0], dabs(a1[1]) * e[1]), dabs(a1[2]) * e[2]), dabs(a1[3]) * e[3]),
-                e[4] * dabs(a1[4]));
-    return mx * Dc[j];
+    const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4];
+    const double m0 = dmax(e0 * dabs(a0[0]), e1 * dabs(a0[1]));
+    const double m1 = dmax(e2 * dabs(a0[2]), e3 * dabs(a0[3]));
+    const double m2 = dmax(dmax(dmax(dmax(dabs(a1[0]) * e0, dabs(a1[1]) * e1), dabs(a1[2]) * e2), dabs(a1[3]) * e3),
+                           e4 * dabs(a1[4]));
+    return sel3(aa, m0, m1, m2) * Dc[j];
   };
   auto arow = [&](int r) __attribute__((always_inline)) {
     const int f = r / 5, k5 = r % 5;
     const double e = Ec[r];
     const double* d = Dc + 3 * f;
-    if (k5 == 4) return (e * dabs(sm.Ap[1][r])) * d[2];
-    return dmax((e * dabs(sm.Ap[0][r])) * d[k5 >> 1], (dabs(sm.Ap[1][r]) * e) * d[2]);
+    const double a0r = sm.Ap[0][r], a1r = sm.Ap[1][r], dk = d[k5 < 4 ? k5 >> 1 : 0], d2 = d[2];
+    const double m4 = (e * dabs(a1r)) * d2;
+    const double m03 = dmax((e * dabs(a0r)) * dk, (dabs(a1r) * e) * d2);
+    return k5 == 4 ? m4 : m03;
   };
   double c_s = 1.0, cm = 0.0;
   // First column pass (D = 1): the raw norms, and H's zero pattern (warm start only): same pattern
