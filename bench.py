@@ -66,7 +66,7 @@ def load_traffic(config_key, kernel):
     for part in kernel.split(" + "):  # every kernel of the solve must be in the measured set
         short = part.split("::")[-1].split("<")[0]  # e.g. wave_kernel
         tmpl = part[part.find("<"):part.find(">") + 1] if "<" in part else ""
-        if short + tmpl not in e.get("kernel", "").replace(" ", ""):
+        if (short + tmpl).replace(" ", "") not in e.get("kernel", "").replace(" ", ""):
             return None
     return e.get("hbm_bytes_per_launch")
 
@@ -247,7 +247,8 @@ def run_rank(args):
             out["roofline"] = None
             out["cpu_baseline"] = None
         else:
-            eff_name = f"mpcqp::wv::scale_kernel<{N}> + mpcqp::wv::wave_kernel<{N}>"
+            ks = 1 if N <= 10 else 0  # KKT form of the launch: Schur (N <= 10, default weights) / Riccati
+            eff_name = f"mpcqp::wv::scale_kernel<{N}> + mpcqp::wv::wave_kernel<{N}, {ks}>"
             flops = algorithmic_flops(N, local_res["iters"], local_res["rho_updates"])  # rank 0's launch
             achieved = flops / (kern_ms * 1e-3) / 1e12
             key = f"N{N}_B{B}_{args.gait}{'_mu' if args.mixed_mu else ''}"
