@@ -204,19 +204,20 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   const bool iv = t < NI;
   const int k = i / 6, c = i % 6;
   // row c of B6 R'^-1: rows 0-2 of B6 are B_w (3 x 12), rows 3-5 dt/m on the matching component
-  // (branch-free: both rows' operands loaded, the lane's case selected after; a per-lane branch ran
-  // the two cases one after the other, each with its own LDS wait)
   double br[12];
-  const int cw = c < 3 ? c : 0, cv = c < 3 ? 0 : c - 3;
 #pragma unroll
   for (int l = 0; l < 4; ++l)
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
       const double* ri = sc.Ri[k][l];
-      const double* bw = sm.Bw[k][cw] + 3 * l;
-      const double sw = (bw[0] * ri[b] + bw[1] * ri[3 + b]) + bw[2] * ri[6 + b];
-      const double sv = dtm * ri[3 * cv + b];
-      br[3 * l + b] = c < 3 ? sw : sv;
+      double s;
+      if (c < 3) {
+        const double* bw = sm.Bw[k][c < 3 ? c : 0] + 3 * l;
+        s = (bw[0] * ri[b] + bw[1] * ri[3 + b]) + bw[2] * ri[6 + b];
+      } else {
+        s = dtm * ri[3 * (c - 3) + b];
+      }
+      br[3 * l + b] = s;
     }
   if (iv)
 #pragma unroll

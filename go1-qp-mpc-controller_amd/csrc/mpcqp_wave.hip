@@ -541,20 +541,16 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     const int kc = kv ? k : 0;
     const int ci = ND * kc + idx, ri = CD * kc + 5 * leg + a, r4 = CD * kc + 5 * leg + 4;
     const int cf = ND * kc + 3 * leg;  // the leg's three variables
-    // (every operand loaded unconditionally at the clamped step, the padding value selected after:
-    // loads under the lane mask became branches, each with its own LDS wait)
-    const double dl = HS.D[ci], ql = HS.q[ci], el = HS.E[ri], e4l = HS.E[r4];
-    const double dfa = HS.D[cf + (a >> 1)], df2 = HS.D[cf + 2];
-    Dv[r] = vv ? dl : 1.0;
+    Dv[r] = vv ? HS.D[ci] : 1.0;
     DI[r] = 1. / Dv[r];
     // update_P then osqp_update_lin_cost: q~ = c (D q) of this tick's gradient
-    Qv[r] = vv ? (mode == 1 ? (HS.qn[ci] * Dv[r]) * c_s : ql) : 0.0;
-    Ev[r] = kv ? el : 1.0;
-    E4[r] = kv ? e4l : 1.0;
+    Qv[r] = vv ? (mode == 1 ? (HS.qn[ci] * Dv[r]) * c_s : HS.q[ci]) : 0.0;
+    Ev[r] = kv ? HS.E[ri] : 1.0;
+    E4[r] = kv ? HS.E[r4] : 1.0;
     // A~ = E A D: row a < 4 has A on fx (a < 2) / fy (a >= 2) and on fz; row 4 on fz
-    AK0[r] = kv ? (ap_of(ri, 0) * Ev[r]) * dfa : 0.0;
-    AK1[r] = kv ? (ap_of(ri, 1) * Ev[r]) * df2 : 0.0;
-    AK4[r] = kv ? (ap_of(r4, 1) * E4[r]) * df2 : 0.0;
+    AK0[r] = kv ? (ap_of(ri, 0) * Ev[r]) * HS.D[cf + (a >> 1)] : 0.0;
+    AK1[r] = kv ? (ap_of(ri, 1) * Ev[r]) * HS.D[cf + 2] : 0.0;
+    AK4[r] = kv ? (ap_of(r4, 1) * E4[r]) * HS.D[cf + 2] : 0.0;
     // bounds (ConvexMpc.cpp:223-245), clipped to +-OSQP_INFTY, scaled by E
     double l4 = fzmin * cont, u4 = fzmax * cont;
     l4 = dmin(dmax(l4, -OSQP_INF), OSQP_INF);
