@@ -158,3 +158,19 @@ def test_product_library_ships_only_the_default_solve():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.DEBUG_LIB_PATH], capture_output=True, text=True).stdout
     exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
     assert _declared_functions() <= exported
+
+
+def test_bench_traffic_matches_the_launched_kernels(tmp_path, monkeypatch):
+    """bench.py's roofline.traffic comes from a PMC pass of exactly the kernels it times: the
+    Schur-form launch (wave_kernel<10, 1>) matches the committed pass, another instantiation or
+    configuration reports null rather than a stale number."""
+    import importlib.util
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    name = "mpcqp::wv::scale_kernel<10> + mpcqp::wv::wave_kernel<10, 1>"
+    t = bench.load_traffic("N10_B4096_trot", name)
+    assert t is not None and t > 0
+    assert bench.load_traffic("N10_B4096_trot", name.replace("<10, 1>", "<10, 0>")) is None
+    assert bench.load_traffic("N20_B4096_trot", name) is None
