@@ -35,6 +35,9 @@ sys.path.insert(0, os.path.join(REPO, "go1-qp-mpc-controller_amd"))
 METRIC = "MPC QP solves/sec (horizon=10, 12 GRF vars) at 1/2/4/8 MI355X vs CPU OSQP"
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, spec
 PARITY_SAMPLE = 4096
+C2_BATCH = 4096           # BASELINE configs[1]: 4096 robots on one MI355X
+C3_BATCH_PER_GPU = 8192   # BASELINE configs[2]: 65536 robots sharded over 8 MI355X
+C3_GPUS = 8
 
 
 def algorithmic_flops(N, iters, rho_updates):
@@ -76,7 +79,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="robots per GPU (configs[1]: 4096; C3: 8192)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="robots per GPU; default 4096 at --gpus 1 (C2, BASELINE configs[1]) and 8192 for "
+                         "--gpus N > 1 (C3, configs[2]: 65536 robots over 8 GPUs)")
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--gait", default="trot", choices=["trot", "stance", "mixed"])
     ap.add_argument("--mixed-mu", action="store_true")
@@ -88,7 +93,10 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-stub", action="store_true",
                     help="TEST ONLY: gloo backend on the CPU, a deterministic stub in place of the device "
                          "solve (exercises the launcher, sharding and all-gather without a GPU)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.batch is None:
+        args.batch = C2_BATCH if args.gpus == 1 else C3_BATCH_PER_GPU
+    return args
 
 
 def oracle_module():
@@ -105,6 +113,20 @@ def parity_of(got, ref):
             "status_equal": bool(np.all(got["status"] == ref["status"])),
             "iters_equal": bool(np.all(got["iters"] == ref["iters"])),
             "iters_equal_frac": float(np.mean(got["iters"] == ref["iters"])) if len(ref) else 1.0}
+
+
+def config_name(N, batch_per_gpu, world, gait, mixed_mu):
+    """BASELINE.json config id of a bench line (None when the line is none of them)."""
+    if N == 10 and gait == "trot" and not mixed_mu:
+        if world == 1 and batch_per_gpu == C2_BATCH:
+            return "C2"
+        if batch_per_gpu == C3_BATCH_PER_GPU:
+            return "C3" if world == C3_GPUS else f"C3 shard size ({world} GPU{'s' if world > 1 else ''})"
+    if N == 20 and gait == "trot" and world == 1 and batch_per_gpu == C2_BATCH:
+        return "C4"
+    if N == 10 and gait == "mixed" and mixed_mu and batch_per_gpu == 8192 and world == 1:
+        return "C5"
+    return None
 
 
 def workload(N, total, gait, mixed_mu):
@@ -168,6 +190,7 @@ def run_rank(args):
             d_res.copy_(stub)
         sync = (lambda: None)
         events = None
+        gevents = None
     else:
         params = mpcqp.default_params(N)
         solver = mpcqp.MpcQpSolver(params, device=local_rank)
@@ -183,6 +206,10 @@ def run_rank(args):
             torch.cuda.synchronize(dev)
         events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(args.steps)]
+        # the all-gather's own span per step (RCCL runs on the current stream; for the gloo stub the
+        # host clock around the blocking call)
+        gevents = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if world > 1 else None
+    gather_host_s = []
 
     def step(k=None):
         if events is not None and k is not None:
@@ -191,7 +218,14 @@ def run_rank(args):
         if events is not None and k is not None:
             events[k][1].record(stream)
         if world > 1:  # the production exchange: u0 of every robot on every rank
-            return allgather_forces(d_res[:, :12].contiguous(), total)
+            tg = time.perf_counter()
+            full = allgather_forces(d_res[:, :12].contiguous(), total)
+            if k is not None:
+                if gevents is not None:
+                    gevents[k].record(stream)
+                else:
+                    gather_host_s.append(time.perf_counter() - tg)
+            return full
         return None
 
     for _ in range(args.warmup):
@@ -213,6 +247,17 @@ def run_rank(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else None
+    gather_ms = None
+    if world > 1:
+        # solve end -> all-gather end of every timed step (max over ranks below)
+        if gevents is not None:
+            gather_ms = float(np.mean([events[k][1].elapsed_time(gevents[k]) for k in range(args.steps)]))
+        else:
+            gather_ms = float(np.mean(gather_host_s)) * 1e3
+        gm = torch.tensor([gather_ms, kern_ms if kern_ms is not None else 0.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(gm, op=dist.ReduceOp.MAX)
+        gather_ms = float(gm[0].item())
+        kern_max_ms = float(gm[1].item())
 
     # whole results of every rank (outside the timed region) for the parity sample
     if world > 1:
@@ -231,7 +276,9 @@ def run_rank(args):
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                "data": "synthetic (seeded Go1 states per SURVEY §8(d); no dataset needed)"}
-        workload_s = (f"Go1 convex-MPC GRF QP, horizon {N} (n={12 * N}, m={20 * N}), {B} robots/GPU, "
+        cname = config_name(N, B, world, args.gait, args.mixed_mu)
+        workload_s = (f"{cname + ': ' if cname else ''}"
+                      f"Go1 convex-MPC GRF QP, horizon {N} (n={12 * N}, m={20 * N}), {B} robots/GPU, "
                       f"{args.gait} gait{', mu~U(0.3,0.9)' if args.mixed_mu else ''}; "
                       f"cold-start OSQP-0.6 settings, adaptive-rho interval 25")
         out["config"] = {"workload": workload_s, "batch_per_gpu": B, "global_batch": total, "horizon": N,
@@ -240,6 +287,12 @@ def run_rank(args):
                          "collective": "RCCL all_gather of u0 per step (mpcqp.distributed.allgather_forces)"
                          if world > 1 else "none"}
         gather_ok = bool(np.array_equal(u0_full, res_all["u0"])) if world > 1 else True
+        if world > 1:
+            out["extras"] = {"allgather_ms": gather_ms, "solve_kernel_ms_max_over_ranks": kern_max_ms,
+                             "allgather_what": ("per timed step: end of the rank's solve -> end of the "
+                                                "all-gather of u0 (HIP events on the solve stream; gloo stub: "
+                                                "host clock), mean over steps, max over ranks"),
+                             "allgather_bytes_per_rank": int(Bl * 12 * 8)}
         if args.cpu_stub:
             exp = stub_results(recs_global)
             out["parity"] = {"gather_exact": bool(np.array_equal(u0_full, exp["u0"]) and gather_ok),
@@ -395,6 +448,37 @@ def extras(args, solver, params, recs_np, states, base_res, pyoracle, dev):
         ref = pyoracle.solve_batch(pyoracle.default_params(10), rec5[idx], nthreads=nthr)
         ent["parity"] = parity_of(g5[idx], ref)
     ex["c5"] = ent
+
+    # -- C3 shard: what one of the 8 GPUs of C3 solves per step (shard 0 of the 65536-robot global
+    # batch), and the batch-size curve of the same seeded global batch (dispatch-tail evidence) --
+    from mpcqp.distributed import shard_range
+    _, rec3 = workload(10, C3_BATCH_PER_GPU * C3_GPUS, "trot", False)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10), device=dev.index) as s3:
+        curve = {}
+        for Bc in (C2_BATCH, C3_BATCH_PER_GPU, 16384, C3_BATCH_PER_GPU * C3_GPUS):
+            s3.reserve(Bc)
+            d3 = torch.from_numpy(np.ascontiguousarray(rec3[:Bc])).to(dev)
+            r3 = torch.zeros((Bc, RD), dtype=torch.float64, device=dev)
+            ms = _timed(lambda: s3.solve_device(d3.data_ptr(), Bc, r3.data_ptr(), 0, sp),
+                        max(3, steps // (1 if Bc <= 16384 else 4)), stream)
+            g3 = res_of(r3)
+            curve[str(Bc)] = {"value": Bc / (ms * 1e-3), "ms_per_step": ms, "mean_iters": float(g3["iters"].mean())}
+            if Bc == C3_BATCH_PER_GPU:
+                b0, b1 = shard_range(C3_BATCH_PER_GPU * C3_GPUS, C3_GPUS, 0)
+                assert (b0, b1) == (0, Bc)
+                ent = {"value": Bc / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms, "batch": Bc, "horizon": 10,
+                       "workload": "C3 shard: robots [0, 8192) of the C3 global batch (65536 trot robots, seed "
+                                   "1000), i.e. rank 0's per-step solve at --gpus 8, on one GPU, no collective",
+                       "mean_iters": float(g3["iters"].mean())}
+                if pyoracle is not None:
+                    idx = np.unique(np.linspace(0, Bc - 1, 512).astype(np.int64))
+                    ref = pyoracle.solve_batch(pyoracle.default_params(10), rec3[idx], nthreads=nthr)
+                    ent["parity"] = parity_of(g3[idx], ref)
+                ex["c3_shard"] = ent
+            del d3, r3
+    ex["batch_scaling"] = {"what": "one GPU, prefixes of the C3 global batch (65536 trot robots, N = 10), "
+                                   "scale_kernel + wave_kernel by HIP events; rate vs batch shows the dispatch tail",
+                           "points": curve}
 
     # -- C4: horizon 20, 4096 trot robots --------------------------------------------------------
     B4 = 4096

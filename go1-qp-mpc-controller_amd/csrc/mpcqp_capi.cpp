@@ -22,6 +22,7 @@ struct mpcqp_handle {
   double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
   size_t work_per = 0;       // doubles per instance the workspace was sized for
+  int* fb = nullptr;         // wave path: Schur -> Riccati fallback list [work_cap + 1] ints
   int path = 0;              // 0 auto (= 3), 3 Riccati wave; debug library only: 1 dense K^-1, 2 Riccati workgroup
   // host wrapper: device buffers, a private stream and two pinned staging chunks
   hipStream_t hstream = nullptr;
@@ -93,7 +94,7 @@ hipError_t occupancy_for(const mpcqp_handle* h, int* per_cu) {
     case 1: return mpcqp::occupancy_any(h->p.horizon, per_cu);
     case 2: return mpcqp::occupancy_riccati_any(h->p.horizon, per_cu);
 #endif
-    default: return mpcqp::occupancy_wave_any(h->p.horizon, per_cu);
+    default: return mpcqp::occupancy_wave_any(h->p, per_cu);
   }
 }
 // (Re)size the per-instance workspace for `batch` instances of the current path.
@@ -103,11 +104,14 @@ hipError_t ensure_workspace(mpcqp_handle* h, int32_t batch, void* stream) {
   if ((size_t)batch <= h->work_cap && per <= h->work_per) return hipSuccess;
   hipError_t e = hipStreamSynchronize((hipStream_t)stream);
   if (e == hipSuccess) e = hipFree(h->work);
+  if (e == hipSuccess) e = hipFree(h->fb);
   h->work = nullptr;
+  h->fb = nullptr;
+  const size_t cap = (size_t)batch > h->work_cap ? (size_t)batch : h->work_cap;
   h->work_cap = 0;
   h->work_per = 0;
-  const size_t cap = (size_t)batch > h->work_cap ? (size_t)batch : h->work_cap;
   if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * per * cap);
+  if (e == hipSuccess) e = hipMalloc(&h->fb, sizeof(int) * (cap + 1));
   if (e == hipSuccess) {
     h->work_cap = cap;
     h->work_per = per;
@@ -126,10 +130,12 @@ bool host_pinned(const void* p) {
   return at.type == hipMemoryTypeHost;
 }
 
-// The host wrappers' private non-blocking stream and pinned staging, created on first use.
+// The host wrappers' private stream and pinned staging, created on first use.  The stream is a
+// BLOCKING one (hipStreamDefault): it is ordered after work the caller queued on the legacy null
+// stream (e.g. hipMemset / torch zeroing of warm slots), as the null-stream wrappers were before.
 hipError_t ensure_host_io(mpcqp_handle* h) {
   hipError_t e = hipSuccess;
-  if (!h->hstream) e = hipStreamCreateWithFlags(&h->hstream, hipStreamNonBlocking);
+  if (!h->hstream) e = hipStreamCreateWithFlags(&h->hstream, hipStreamDefault);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) {
     if (!h->pin[i]) e = hipHostMalloc((void**)&h->pin[i], PIN_CHUNK, hipHostMallocDefault);
     if (e == hipSuccess && !h->pin_ev[i]) e = hipEventCreateWithFlags(&h->pin_ev[i], hipEventDisableTiming);
@@ -245,6 +251,7 @@ int32_t mpcqp_destroy(mpcqp_handle* h) {
   if (!h) return MPCQP_ERR_INVALID_ARG;
   DeviceGuard dg(h->device);
   (void)hipFree(h->work);
+  (void)hipFree(h->fb);
   (void)hipFree(h->d_recs);
   (void)hipFree(h->d_res);
   (void)hipFree(h->d_sol);
@@ -281,6 +288,7 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   a.trace = d_trace;
   a.trace_cap = d_trace ? trace_cap : 0;
   a.wstate = d_state;
+  a.fallback = h->fb;
   a.grid = batch;
   a.stream = stream;
   a.p = h->p;
@@ -523,6 +531,39 @@ int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path) {
   }
   h->slots = per_cu * h->cus;
   return MPCQP_OK;
+}
+
+int32_t mpcqp_debug_scale_image_doubles(int32_t horizon) {
+  if (horizon < 1 || horizon > MPCQP_MAX_HORIZON) return 0;
+  return mpcqp::scale_image_doubles(horizon);
+}
+
+int32_t mpcqp_debug_scale_image_device(mpcqp_handle* h, const double* d_records, int32_t batch, double* d_state,
+                                       double* d_img, void* stream) {
+#ifdef MPCQP_DEBUG_PATHS
+  if (!h || batch < 0 || (batch > 0 && (!d_records || !d_img))) return MPCQP_ERR_INVALID_ARG;
+  if (batch == 0) return MPCQP_OK;
+  DeviceGuard dg(h->device);
+  hipError_t e = dg.err;
+  if (e != hipSuccess) return set_hip_error(h, e, "hipSetDevice");
+  e = ensure_workspace(h, batch, stream);  // (the fallback list the kernel resets)
+  if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
+  mpcqp::LaunchArgs a;
+  memset(&a, 0, sizeof(a));
+  a.recs = d_records;
+  a.batch = batch;
+  a.work = d_img;
+  a.wstate = d_state;
+  a.fallback = h->fb;
+  a.stream = stream;
+  a.p = h->p;
+  e = mpcqp::launch_scale_any(a);
+  if (e != hipSuccess) return set_hip_error(h, e, "scale_kernel launch");
+  return MPCQP_OK;
+#else
+  (void)h; (void)d_records; (void)batch; (void)d_state; (void)d_img; (void)stream;
+  return MPCQP_ERR_INVALID_ARG;  // libmpcqp_debug.so only
+#endif
 }
 
 int32_t mpcqp_debug_wave_selftest(double* d_out, void* stream) {

@@ -18,6 +18,7 @@ struct LaunchArgs {
   double* trace;
   int trace_cap;
   double* wstate;  // warm-start slots [batch][warm_state_doubles(N)] (wave path) or nullptr
+  int* fallback;   // wave path: [batch + 1] ints, the Schur -> Riccati fallback list (handle-owned)
   int grid;
   void* stream;
   mpcqp_params p;
@@ -29,7 +30,9 @@ hipError_t launch_build_any(const LaunchArgs& a, double* P, double* q, double* l
 // The solve: scale_kernel + one-wave-per-robot Riccati wave_kernel (mpcqp_wave.hip), horizons
 // 1..WAVE_MAX_HORIZON
 hipError_t launch_wave_any(const LaunchArgs& a);
-hipError_t occupancy_wave_any(int horizon, int* blocks);
+hipError_t occupancy_wave_any(const mpcqp_params& p, int* blocks);
+// grid of the Riccati fallback launch after the Schur-form wave kernel (grid-stride over its list)
+constexpr int FALLBACK_GRID = 1024;
 hipError_t wave_selftest(double* d_out, void* stream);
 hipError_t launch_scale_any(const LaunchArgs& a);  // scale_kernel alone (the image in a.work)
 constexpr int WAVE_MAX_HORIZON = 20;

@@ -56,7 +56,8 @@ namespace wv {
 template <int N>
 __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kernel(const double* __restrict__ recs, int batch,
                                                                  double* __restrict__ wstate,
-                                                                 double* __restrict__ img, mpcqp_params p) {
+                                                                 double* __restrict__ img, mpcqp_params p,
+                                                                 int* __restrict__ fb) {
   using C = Cfg<N>;
   using SC = ScaleCfg<N>;
   using WL = WarmLayout<N>;
@@ -66,6 +67,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   const int inst = blockIdx.x;
   if (inst >= batch) return;
   const int t = threadIdx.x;
+  if (inst == 0 && t == 0) fb[0] = 0;  // wave_kernel's fallback list starts empty (stream order)
   {
     const double* rg = recs + (size_t)inst * C::REC;
     int bad = 0;
@@ -399,18 +401,19 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
 
 // KS: the KKT solve.  0 = Riccati recursion (chains over the horizon, factors on MFMA; every N),
 // 1 = impulse-space Schur form (mpcqp_schur.h; N <= 10, nonnegative state weights).
+// The solve of robot `inst` by one wave (the kernels below: one robot per workgroup, or the
+// Riccati fallback's list of robots).  KS = 1 robots whose G_k is (nearly) singular append
+// themselves to fb (fb[0] = count, fb[1..]) and return without writing anything: the fallback
+// kernel solves them with KS = 0.
 template <int N, int KS>
-__global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ recs, int batch,
-                                                     mpcqp_result* __restrict__ results,
-                                                     double* __restrict__ solution, double* __restrict__ trace,
-                                                     int trace_cap, double* __restrict__ wstate,
-                                                     const double* __restrict__ img, mpcqp_params p) {
+__device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, const double* __restrict__ recs,
+                                           mpcqp_result* __restrict__ results, double* __restrict__ solution,
+                                           double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
+                                           const double* __restrict__ img, const mpcqp_params& p,
+                                           int* __restrict__ fb) {
   using C = Cfg<N>;
   using WL = WarmLayout<N>;
   constexpr int n = C::n, m = C::m, R = C::R;
-  __shared__ WSmem<N, KS> sm;
-  const int inst = blockIdx.x;
-  if (inst >= batch) return;
   const int t = threadIdx.x;
   const int q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
   const bool av = a < 3;
@@ -499,7 +502,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   for (int j = t; j < n; j += NT) {
     HS.D[j] = im[SI::D + j];
     HS.q[j] = im[SI::Q + j];
-    if (mode == 1) HS.qn[j] = im[SI::QN + j];
+    if (mode != 0) HS.qn[j] = im[SI::QN + j];
   }
   for (int r = t; r < m; r += NT) HS.E[r] = im[SI::E + r];
   // Warm start (A1RobotControl.h:67 member solver, :522-538): the slot of the previous tick.
@@ -543,8 +546,9 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
     const int cf = ND * kc + 3 * leg;  // the leg's three variables
     Dv[r] = vv ? HS.D[ci] : 1.0;
     DI[r] = 1. / Dv[r];
-    // update_P then osqp_update_lin_cost: q~ = c (D q) of this tick's gradient
-    Qv[r] = vv ? (mode == 1 ? (HS.qn[ci] * Dv[r]) * c_s : HS.q[ci]) : 0.0;
+    // warm ticks end with osqp_update_lin_cost (A1RobotControl.cpp:533, after updateHessianMatrix's
+    // update_P or re-init): q~ = c (D q) of this tick's gradient; a cold setup scales q pass by pass
+    Qv[r] = vv ? (mode != 0 ? (HS.qn[ci] * Dv[r]) * c_s : HS.q[ci]) : 0.0;
     Ev[r] = kv ? HS.E[ri] : 1.0;
     E4[r] = kv ? HS.E[r4] : 1.0;
     // A~ = E A D: row a < 4 has A on fx (a < 2) / fy (a >= 2) and on fz; row 4 on fz
@@ -710,6 +714,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   };
   double rho = rho0, rinv = 1. / rho0, pri_res = 0.0, dua_res = 0.0;
   int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
+  bool handoff = false;  // KS = 1: this robot goes to the Riccati fallback (see schur_factor)
   bool need_factor = true;
   int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
   for (int iter = 1; iter <= p.max_iter; ++iter) {
@@ -755,8 +760,18 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
       }
       wave_sync();
       if constexpr (KS == 0) factorize_mfma<N>(sm, p, A, cost_c, dtm, Q2J);
-      else schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI,
-                              [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; });
+      else {
+        bool degen = false;
+        schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI,
+                           [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; }, degen);
+        // G_k = B6_k R'^-1 B6_k' (nearly) singular: collinear or coincident feet make B6_k rank
+        // deficient (the reference QP is still strictly convex through R).  The Riccati form
+        // (KS = 0) solves this robot instead; nothing of it has been written yet.
+        if (degen) {
+          handoff = true;
+          break;
+        }
+      }
       wave_sync();
 #ifdef MPCQP_REPEAT_FACTOR
      }
@@ -1192,6 +1207,13 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   }
 
   WV_MARK(20);
+  if (handoff) {  // nothing of this robot has been written: the fallback kernel solves it
+    if (t == 0) {
+      const int j = atomicAdd(fb, 1);
+      fb[1 + j] = inst;
+    }
+    return;
+  }
   if (ws) {  // the solver persists: scaling, scaled data, iterates and rho for the next tick
     if (t == 0) {
       ws[WL::FLAG] = 1.0;
@@ -1282,6 +1304,37 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
   }
 }
 
+template <int N, int KS>
+__global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ recs, int batch,
+                                                     mpcqp_result* __restrict__ results,
+                                                     double* __restrict__ solution, double* __restrict__ trace,
+                                                     int trace_cap, double* __restrict__ wstate,
+                                                     const double* __restrict__ img, mpcqp_params p,
+                                                     int* __restrict__ fb) {
+  __shared__ WSmem<N, KS> sm;
+  const int inst = blockIdx.x;
+  if (inst >= batch) return;
+  wave_solve<N, KS>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb);
+}
+
+// The robots wave_kernel<N, 1> handed over (fb[0] of them at fb[1..]), by the Riccati form; a
+// grid-stride loop over the list, so any grid size covers any count (0: every wave exits at once).
+template <int N>
+__global__ __launch_bounds__(NT, 1) void wave_fallback_kernel(const double* __restrict__ recs,
+                                                              mpcqp_result* __restrict__ results,
+                                                              double* __restrict__ solution,
+                                                              double* __restrict__ trace, int trace_cap,
+                                                              double* __restrict__ wstate,
+                                                              const double* __restrict__ img, mpcqp_params p,
+                                                              const int* __restrict__ fb) {
+  __shared__ WSmem<N, 0> sm;
+  const int cnt = fb[0];
+  for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
+    wave_solve<N, 0>(fb[1 + j], sm, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr);
+    wave_sync();
+  }
+}
+
 // Self-test of the cross-lane primitives (mv12 broadcast lanes, rmove directions): out[64*k + lane].
 __global__ void wave_selftest_kernel(double* out) {
   const int t = threadIdx.x;
@@ -1311,30 +1364,40 @@ static bool schur_ok(const mpcqp_params& p) {
 }
 template <int N>
 static hipError_t launch_wave(const LaunchArgs& a) {
+  if (!a.fallback) return hipErrorInvalidValue;
   hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
-                     a.recs, a.batch, a.wstate, a.work, a.p);
+                     a.recs, a.batch, a.wstate, a.work, a.p, a.fallback);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if constexpr (N <= 10) {
     if (schur_ok(a.p)) {
       hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs,
-                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p);
+                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      // the robots with (nearly) singular G_k, if any (an empty list costs one short launch)
+      const int grid = a.batch < FALLBACK_GRID ? a.batch : FALLBACK_GRID;
+      hipLaunchKernelGGL((wv::wave_fallback_kernel<N>), dim3(grid), dim3(wv::NT), 0, (hipStream_t)a.stream,
+                         a.recs, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
       return hipGetLastError();
     }
   }
   hipLaunchKernelGGL((wv::wave_kernel<N, 0>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs, a.batch,
-                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p);
+                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
   return hipGetLastError();
 }
 template <int N>
 static hipError_t launch_scale(const LaunchArgs& a) {
+  if (!a.fallback) return hipErrorInvalidValue;
   hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
-                     a.recs, a.batch, a.wstate, a.work, a.p);
+                     a.recs, a.batch, a.wstate, a.work, a.p, a.fallback);
   return hipGetLastError();
 }
+// occupancy of the wave kernel a handle with these parameters launches (the KS choice of launch_wave)
 template <int N>
-static hipError_t occupancy_wave(int* blocks) {
-  if constexpr (N <= 10) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wv::wave_kernel<N, 1>, wv::NT, 0);
+static hipError_t occupancy_wave(const mpcqp_params& p, int* blocks) {
+  if constexpr (N <= 10)
+    if (schur_ok(p)) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wv::wave_kernel<N, 1>, wv::NT, 0);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wv::wave_kernel<N, 0>, wv::NT, 0);
 }
 
@@ -1361,10 +1424,10 @@ hipError_t launch_scale_any(const LaunchArgs& a) {
     default: return hipErrorInvalidValue;
   }
 }
-hipError_t occupancy_wave_any(int horizon, int* blocks) {
-  switch (horizon) {
+hipError_t occupancy_wave_any(const mpcqp_params& p, int* blocks) {
+  switch (p.horizon) {
 #define CASE(K) \
-  case K: return occupancy_wave<K>(blocks);
+  case K: return occupancy_wave<K>(p, blocks);
     MPCQP_WAVE_FOR_EACH_N(CASE)
 #undef CASE
     default: return hipErrorInvalidValue;

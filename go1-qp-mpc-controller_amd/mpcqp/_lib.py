@@ -105,6 +105,7 @@ EXPORTED = [
     "mpcqp_warm_state_size", "mpcqp_solve_batch_warm_device",
     "mpcqp_balance_default_params", "mpcqp_balance_solve_device", "mpcqp_assemble_records_device",
     "mpcqp_balance_solve_host", "mpcqp_solve_batch_warm_host",
+    "mpcqp_debug_scale_image_doubles", "mpcqp_debug_scale_image_device",
 ]
 
 _libs = {}
@@ -157,6 +158,10 @@ def load(debug=False):
     L.mpcqp_debug_set_solver.restype = i32
     L.mpcqp_debug_wave_selftest.argtypes = [vp, vp]
     L.mpcqp_debug_wave_selftest.restype = i32
+    L.mpcqp_debug_scale_image_doubles.argtypes = [i32]
+    L.mpcqp_debug_scale_image_doubles.restype = i32
+    L.mpcqp_debug_scale_image_device.argtypes = [vp, vp, i32, vp, vp, vp]
+    L.mpcqp_debug_scale_image_device.restype = i32
     L.mpcqp_joint_torques_device.argtypes = [vp, vp, i32, vp, vp, vp]
     L.mpcqp_joint_torques_device.restype = i32
     L.mpcqp_warm_state_size.argtypes = [i32]

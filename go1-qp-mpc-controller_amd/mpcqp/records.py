@@ -46,7 +46,8 @@ class RobotStates:
     mu: np.ndarray = None             # [B] (ConvexMpc.cpp:8: 0.3)
     fz_min: float = 0.0               # ConvexMpc.cpp:223
     fz_max: float = 180.0             # ConvexMpc.cpp:224
-    mpc_dt: float = MPC_DT
+    mpc_dt: float = MPC_DT            # (RobotControl.compute_grf uses its own mpc_dt / dt, see there)
+    stance_leg_control_type: np.ndarray = None  # [B] or scalar: 0 QP balance, 1 MPC (None: all MPC)
 
     @property
     def batch(self):

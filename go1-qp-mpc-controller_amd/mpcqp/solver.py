@@ -81,6 +81,16 @@ class MpcQpSolver:
                                                     d_solution or None, stream or None),
               self._h, "mpcqp_solve_batch_warm_device", self._L)
 
+    @property
+    def scale_image_size(self):
+        return int(self._L.mpcqp_debug_scale_image_doubles(self.params.horizon))
+
+    def scale_image_device(self, d_records, batch, d_state, d_img, stream=0):
+        """Debug library: scale_kernel's image alone (include/mpcqp_debug.h); d_state 0 = cold."""
+        check(self._L.mpcqp_debug_scale_image_device(self._h, d_records, int(batch), d_state or None, d_img,
+                                                     stream or None), self._h, "mpcqp_debug_scale_image_device",
+              self._L)
+
     def solve_device_trace(self, d_records, batch, d_results, d_solution, d_trace, trace_cap, stream=0):
         check(self._L.mpcqp_debug_solve_trace_device(self._h, d_records, int(batch), d_results,
                                                      d_solution or None, d_trace, int(trace_cap),

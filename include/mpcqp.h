@@ -157,7 +157,11 @@ int32_t mpcqp_solve_batch_warm_device(mpcqp_handle* h, const double* d_records, 
                                       mpcqp_result* d_results, double* d_solution, void* stream);
 
 /* Host-pointer convenience wrapper (copies in, solves, copies out, synchronizes) on a stream of the
- * handle's own.  Pinned host buffers (hipHostMalloc / registered) move by one DMA each way;
+ * handle's own.  That stream is a blocking stream: it waits for work queued before the call on the
+ * legacy NULL stream (zeroing warm slots with hipMemset(..) / on torch's default stream is ordered
+ * before the solve), but NOT for work on other non-blocking streams — synchronize those first.  One
+ * handle must not run a device-pointer solve on another stream concurrently with a host-wrapper
+ * call (they share the handle's workspace).  Pinned host buffers (hipHostMalloc / registered) move by one DMA each way;
  * pageable ones through two pinned 2-MiB staging chunks of the handle, host copies overlapping the
  * DMA.  Not for concurrent use of one handle from several threads. */
 int32_t mpcqp_solve_batch_host(mpcqp_handle* h, const double* h_records, int32_t batch,

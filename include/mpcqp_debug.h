@@ -35,6 +35,18 @@ int32_t mpcqp_solve_threads(int32_t horizon);
  * inputs.  The product libmpcqp.so returns MPCQP_ERR_INVALID_ARG for 1 and 2. */
 int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path);
 
+/* The scaling image scale_kernel hands to wave_kernel (OSQP scale_data of the robot's QP, and for
+ * warm slots the update_P / re-init branch): per robot mpcqp_debug_scale_image_doubles(N) doubles
+ *   [0, 12N) D, [12N, 32N) E, [32N, 44N) q~ (cold / re-init: c D q; update_P: the previous tick's
+ *   scaled gradient re-scaled), [44N, 56N) this tick's raw gradient q (warm slots), [56N] c,
+ *   [56N + 1] branch (0 cold, 1 osqp_update_P, 2 OsqpEigen re-init).
+ * d_state: warm slots as for mpcqp_solve_batch_warm_device, or NULL (cold).  Note that the pass
+ * records H's zero pattern into the slots (as the solve's own pass does): run it on a copy.
+ * libmpcqp_debug.so only (the product library returns MPCQP_ERR_INVALID_ARG). */
+int32_t mpcqp_debug_scale_image_doubles(int32_t horizon);
+int32_t mpcqp_debug_scale_image_device(mpcqp_handle* h, const double* d_records, int32_t batch, double* d_state,
+                                       double* d_img, void* stream);
+
 /* Cross-lane primitive self-test of the wave path: writes 6 x 64 doubles to d_out (device). */
 int32_t mpcqp_debug_wave_selftest(double* d_out, void* stream);
 

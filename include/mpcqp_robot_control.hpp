@@ -20,6 +20,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -126,6 +127,65 @@ struct Mat {
   }
 };
 using Matrix34 = Mat<3, MPCQP_NUM_LEG>;
+
+// Heap-backed row-major binary64 matrix for the large formulation members (B_qp is 13N x 12N).
+struct DMat {
+  int r = 0, c = 0;
+  std::vector<double> a;
+  DMat() = default;
+  DMat(int rows_, int cols_) : r(rows_), c(cols_), a((size_t)rows_ * cols_, 0.0) {}
+  int rows() const { return r; }
+  int cols() const { return c; }
+  double& operator()(int i, int j) { return a[(size_t)i * c + j]; }
+  const double& operator()(int i, int j) const { return a[(size_t)i * c + j]; }
+  double* data() { return a.data(); }
+  const double* data() const { return a.data(); }
+};
+
+// A public data member of the reference's ConvexMpc whose value is produced on first read after
+// calculate_qp_mats (ConvexMpc.h:77-92): the shim computes hessian / gradient on the device and
+// A_qp / B_qp / linear_constraints on the host only when the caller actually reads them, so a tick
+// that only needs the solve moves no dense matrix across PCIe.  Reads look like the member's
+// (v[i], v.size(), range-for, v.data(), implicit conversion to the value type).
+template <class T>
+class Lazy {
+ public:
+  using value_type = T;
+  const T& get() const {
+    if (!valid_) {
+      if (!fill_) throw std::logic_error("ConvexMpc: member read before calculate_qp_mats");
+      fill_(val_);
+      valid_ = true;
+    }
+    return val_;
+  }
+  operator const T&() const { return get(); }
+  // (member templates: each exists only for value types that have the operation)
+  template <class U = T>
+  auto operator[](size_t i) const -> decltype(std::declval<const U&>()[i]) { return get()[i]; }
+  template <class U = T>
+  auto operator()(int i, int j) const -> decltype(std::declval<const U&>()(i, j)) { return get()(i, j); }
+  template <class U = T>
+  auto size() const -> decltype(std::declval<const U&>().size()) { return get().size(); }
+  const double* data() const { return get().data(); }
+  template <class U = T>
+  auto begin() const -> decltype(std::declval<const U&>().begin()) { return get().begin(); }
+  template <class U = T>
+  auto end() const -> decltype(std::declval<const U&>().end()) { return get().end(); }
+  bool computed() const { return valid_; }  // tests: has this member been materialised?
+  // (internal) the producer for the current formulation
+  template <class F>
+  void reset(T init, F&& fill) {
+    val_ = std::move(init);
+    valid_ = false;
+    fill_ = std::forward<F>(fill);
+  }
+
+ private:
+  mutable T val_{};
+  mutable bool valid_ = false;
+  std::function<void(T&)> fill_;
+};
 
 namespace detail {
 
@@ -235,11 +295,6 @@ class ConvexMpc {
     for (int i = 0; i < MPCQP_STATE_DIM; ++i) q[i] = q_weights_[i];
     for (int i = 0; i < MPCQP_NUM_DOF; ++i) r[i] = r_weights_[i];
     slot_ = detail::build_slot<N>(device, q, r);
-    hessian.assign((size_t)n * n, 0.0);
-    gradient.assign(n, 0.0);
-    lb.assign(m, 0.0);
-    ub.assign(m, 0.0);
-    linear_constraints.assign((size_t)m * n, 0.0);
     reset();
   }
   ConvexMpc(const ConvexMpc&) = delete;
@@ -254,9 +309,14 @@ class ConvexMpc {
     A_mat_d.setZero();
     B_mat_d.setZero();
     B_mat_d_list.setZero();
-    std::fill(gradient.begin(), gradient.end(), 0.0);
-    std::fill(lb.begin(), lb.end(), 0.0);
-    std::fill(ub.begin(), ub.end(), 0.0);
+    lb.assign(m, 0.0);
+    ub.assign(m, 0.0);
+    const auto zeros = [](size_t k) { return [k](std::vector<double>& v) { v.assign(k, 0.0); }; };
+    hessian.reset({}, zeros((size_t)n * n));  // the reference's zero-filled members (:70-108)
+    gradient.reset({}, zeros(n));
+    linear_constraints.reset({}, zeros((size_t)m * n));
+    A_qp.reset(DMat(), [](DMat& d) { d = DMat(13 * N, 13); });
+    B_qp.reset(DMat(), [](DMat& d) { d = DMat(13 * N, MPCQP_NUM_DOF * N); });
   }
 
   template <class Vec3>
@@ -310,7 +370,10 @@ class ConvexMpc {
     ++step_;
   }
 
-  // ConvexMpc.cpp:158-245.  State needs mpc_states (13), mpc_states_d (13N) and contacts[4].
+  // ConvexMpc.cpp:158-245.  State needs mpc_states (13), mpc_states_d (13N) and contacts[4].  The
+  // record for the solve is complete on return and lb / ub are filled; hessian and gradient (device
+  // formulation, mpcqp_build_qp_device), A_qp / B_qp and linear_constraints (host) are produced
+  // when first read.
   template <class State>
   void calculate_qp_mats(const State& state) {
     for (int i = 0; i < N; ++i) feet_of_block(i, &rec_[MPCQP_REC_FEET(N) + 12 * i]);
@@ -322,20 +385,80 @@ class ConvexMpc {
     rec_[MPCQP_REC_MU] = mu;
     rec_[MPCQP_REC_FZMIN] = fz_min;
     rec_[MPCQP_REC_FZMAX] = fz_max;
-    build_on_device();
-    std::fill(linear_constraints.begin(), linear_constraints.end(), 0.0);
-    for (int f = 0; f < MPCQP_NUM_LEG * N; ++f) {  // ConvexMpc.cpp:46-58
-      double* A = linear_constraints.data();
-      A[(size_t)(5 * f + 0) * n + 3 * f + 0] = 1;
-      A[(size_t)(5 * f + 1) * n + 3 * f + 0] = 1;
-      A[(size_t)(5 * f + 2) * n + 3 * f + 1] = 1;
-      A[(size_t)(5 * f + 3) * n + 3 * f + 1] = 1;
-      A[(size_t)(5 * f + 4) * n + 3 * f + 2] = 1;
-      A[(size_t)(5 * f + 0) * n + 3 * f + 2] = mu;
-      A[(size_t)(5 * f + 1) * n + 3 * f + 2] = -mu;
-      A[(size_t)(5 * f + 2) * n + 3 * f + 2] = mu;
-      A[(size_t)(5 * f + 3) * n + 3 * f + 2] = -mu;
-    }
+    for (int i = 0; i < N; ++i)  // ConvexMpc.cpp:223-245 (the current contacts over the horizon)
+      for (int l = 0; l < MPCQP_NUM_LEG; ++l) {
+        const double c = rec_[MPCQP_REC_CONTACTS + l];
+        double* lo = &lb[MPCQP_CONSTRAINT_DIM * i + 5 * l];
+        double* up = &ub[MPCQP_CONSTRAINT_DIM * i + 5 * l];
+        lo[0] = 0; lo[1] = -MPCQP_OSQP_INFTY; lo[2] = 0; lo[3] = -MPCQP_OSQP_INFTY; lo[4] = fz_min * c;
+        up[0] = MPCQP_OSQP_INFTY; up[1] = 0; up[2] = MPCQP_OSQP_INFTY; up[3] = 0; up[4] = fz_max * c;
+      }
+    // one device round trip fills both device members, whichever is read first
+    auto dev = std::make_shared<std::vector<double>>();
+    auto fetch = [this, dev, rec = rec_](int which, std::vector<double>& out) {
+      if (dev->empty()) {  // (the record as of this call: later setters do not leak into it)
+        std::vector<double> H((size_t)n * n), g(n);
+        build_on_device(rec, H.data(), g.data());
+        dev->swap(H);
+        dev->insert(dev->end(), g.begin(), g.end());
+      }
+      if (which == 0) out.assign(dev->begin(), dev->begin() + (size_t)n * n);
+      else out.assign(dev->begin() + (size_t)n * n, dev->end());
+    };
+    hessian.reset({}, [fetch](std::vector<double>& v) { fetch(0, v); });
+    gradient.reset({}, [fetch](std::vector<double>& v) { fetch(1, v); });
+    const double mu_ = mu;
+    linear_constraints.reset({}, [mu_](std::vector<double>& A) {  // ConvexMpc.cpp:46-58, dense
+      A.assign((size_t)m * n, 0.0);
+      for (int f = 0; f < MPCQP_NUM_LEG * N; ++f) {
+        A[(size_t)(5 * f + 0) * n + 3 * f + 0] = 1;
+        A[(size_t)(5 * f + 1) * n + 3 * f + 0] = 1;
+        A[(size_t)(5 * f + 2) * n + 3 * f + 1] = 1;
+        A[(size_t)(5 * f + 3) * n + 3 * f + 1] = 1;
+        A[(size_t)(5 * f + 4) * n + 3 * f + 2] = 1;
+        A[(size_t)(5 * f + 0) * n + 3 * f + 2] = mu_;
+        A[(size_t)(5 * f + 1) * n + 3 * f + 2] = -mu_;
+        A[(size_t)(5 * f + 2) * n + 3 * f + 2] = mu_;
+        A[(size_t)(5 * f + 3) * n + 3 * f + 2] = -mu_;
+      }
+    });
+    // A_qp / B_qp by the reference's recurrence (ConvexMpc.cpp:184-202), from A_mat_d and the
+    // B_mat_d_list the caller stored
+    const Mat<13, 13> Ad = A_mat_d;
+    const Mat<13 * N, 12> Bl = B_mat_d_list;
+    auto aqp = std::make_shared<DMat>();
+    auto make_aqp = [aqp, Ad]() -> const DMat& {
+      if (aqp->rows() == 0) {
+        *aqp = DMat(13 * N, 13);
+        for (int i = 0; i < N; ++i)
+          for (int r = 0; r < 13; ++r)
+            for (int c = 0; c < 13; ++c) {
+              if (i == 0) { (*aqp)(r, c) = Ad(r, c); continue; }
+              double s = 0.0;
+              for (int k = 0; k < 13; ++k) s += (*aqp)(13 * (i - 1) + r, k) * Ad(k, c);
+              (*aqp)(13 * i + r, c) = s;
+            }
+      }
+      return *aqp;
+    };
+    A_qp.reset(DMat(), [make_aqp](DMat& d) { d = make_aqp(); });
+    B_qp.reset(DMat(), [make_aqp, Bl](DMat& d) {
+      const DMat& Aq = make_aqp();
+      d = DMat(13 * N, MPCQP_NUM_DOF * N);
+      for (int i = 0; i < N; ++i)
+        for (int j = 0; j <= i; ++j)
+          for (int r = 0; r < 13; ++r)
+            for (int c = 0; c < 12; ++c) {
+              double s;
+              if (i == j) {
+                s = Bl(13 * j + r, c);
+              } else {
+                s = 0.0;
+                for (int k = 0; k < 13; ++k) s += Aq(13 * (i - j - 1) + r, k) * Bl(13 * j + k, c);
+              }
+              d(13 * i + r, 12 * j + c) = s;
+            }
+    });
   }
 
   // the record handed to the solve path (inputs of calculate_qp_mats + the solve)
@@ -348,11 +471,13 @@ class ConvexMpc {
   double mu, fz_min, fz_max;
   Mat<13, 13> A_mat_c, A_mat_d;
   Mat<13, 12> B_mat_c, B_mat_d;
-  Mat<13 * N, 12> B_mat_d_list;            // block i: B_d of horizon step i (written by the caller)
-  std::vector<double> hessian;             // dense row-major n x n (reference: sparseView of it)
-  std::vector<double> gradient;            // n
-  std::vector<double> lb, ub;              // m
-  std::vector<double> linear_constraints;  // dense row-major m x n
+  Mat<13 * N, 12> B_mat_d_list;                  // block i: B_d of horizon step i (written by the caller)
+  Lazy<DMat> A_qp;                               // 13N x 13 (ConvexMpc.h:77)
+  Lazy<DMat> B_qp;                               // 13N x 12N (ConvexMpc.h:78)
+  Lazy<std::vector<double>> hessian;             // dense row-major n x n (reference: sparseView of it)
+  Lazy<std::vector<double>> gradient;            // n
+  std::vector<double> lb, ub;                    // m
+  Lazy<std::vector<double>> linear_constraints;  // dense row-major m x n
 
  private:
   // Feet of horizon step i from B_mat_d_list block i.  The block the reference's loop stores is the
@@ -389,8 +514,20 @@ class ConvexMpc {
       feet[3 * l + 1] = 0.5 * (S[2] - S[6]);
       feet[3 * l + 2] = 0.5 * (S[3] - S[1]);
     }
+    // rows 6-8 must be exactly what those feet give with this robot's I_w (a block built with
+    // another rotation / inertia, or not skew-symmetric through I_w, is rejected, not re-read)
+    Mat<13, 12> Bc;
+    detail::b_mat_c(rec_[MPCQP_REC_MASS], Iwinv_, feet, Bc);
+    double scale = 0.0;
+    for (int r = 6; r < 9; ++r)
+      for (int c = 0; c < 12; ++c) scale = std::fmax(scale, std::fabs(blk(r, c)));
+    for (int r = 6; r < 9; ++r)
+      for (int c = 0; c < 12; ++c)
+        if (std::fabs(Bc(r, c) * dt - blk(r, c)) > 1e-9 * scale + 1e-300)
+          throw std::invalid_argument("ConvexMpc: B_mat_d_list block " + std::to_string(i) +
+                                      " rows 6-8 are not I_w^-1 [r]x dt of this robot for any feet r");
   }
-  void build_on_device();
+  void build_on_device(const std::vector<double>& rec, double* H, double* g) const;
 
   int device_ = 0;
   detail::BuildSlot<N>* slot_ = nullptr;
@@ -403,17 +540,17 @@ class ConvexMpc {
   int step_ = 0;
 };
 
+// The formulation of one record on the device (shared staging of the weights' BuildSlot, held for
+// the round trip): H (n x n) and g (n) to the host.
 template <int N>
-void ConvexMpc<N>::build_on_device() {
+void ConvexMpc<N>::build_on_device(const std::vector<double>& rec, double* H, double* g) const {
   detail::BuildSlot<N>& s = *slot_;
   std::lock_guard<std::mutex> lk(s.mu);
   DeviceScope ds(s.device);
-  hip_ok(hipMemcpy(s.d_rec, rec_.data(), sizeof(double) * rec_.size(), hipMemcpyHostToDevice), "hipMemcpy");
+  hip_ok(hipMemcpy(s.d_rec, rec.data(), sizeof(double) * rec.size(), hipMemcpyHostToDevice), "hipMemcpy");
   throw_on(mpcqp_build_qp_device(s.h, s.d_rec, 1, s.d_P, s.d_q, s.d_l, s.d_u, nullptr), s.h, "mpcqp_build_qp_device");
-  hip_ok(hipMemcpy(hessian.data(), s.d_P, sizeof(double) * hessian.size(), hipMemcpyDeviceToHost), "hipMemcpy");
-  hip_ok(hipMemcpy(gradient.data(), s.d_q, sizeof(double) * n, hipMemcpyDeviceToHost), "hipMemcpy");
-  hip_ok(hipMemcpy(lb.data(), s.d_l, sizeof(double) * m, hipMemcpyDeviceToHost), "hipMemcpy");
-  hip_ok(hipMemcpy(ub.data(), s.d_u, sizeof(double) * m, hipMemcpyDeviceToHost), "hipMemcpy");
+  hip_ok(hipMemcpy(H, s.d_P, sizeof(double) * n * n, hipMemcpyDeviceToHost), "hipMemcpy");
+  hip_ok(hipMemcpy(g, s.d_q, sizeof(double) * n, hipMemcpyDeviceToHost), "hipMemcpy");
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -431,6 +568,19 @@ struct Go1InertiaOf {
   template <class S> static const auto& get(const S& s) { return s.go1_trunk_inertia; }
 };
 
+// state.stance_leg_control_type (A1CtrlStates.h / Go1CtrlStates.hpp: 0 = QP balance, 1 = MPC), or
+// 1 for a state type without the field (an MPC-only caller)
+template <class S, class = void>
+struct has_control_type : std::false_type {};
+template <class S>
+struct has_control_type<S, std::void_t<decltype(std::declval<const S&>().stance_leg_control_type)>>
+    : std::true_type {};
+template <class S>
+int control_type_of(const S& s) {
+  if constexpr (has_control_type<S>::value) return (int)s.stance_leg_control_type;
+  else return 1;
+}
+
 template <class InertiaOf, int N = 10>
 class RobotControlT {
  public:
@@ -442,9 +592,10 @@ class RobotControlT {
     throw_on(mpcqp_create(&params_, device, &h_), nullptr, "mpcqp_create");
   }
   ~RobotControlT() {
-    if (d_state_) {
+    if (d_state_ || d_gather_) {
       DeviceScope ds(device_);
       (void)hipFree(d_state_);
+      (void)hipFree(d_gather_);
     }
     if (h_) mpcqp_destroy(h_);
   }
@@ -517,23 +668,66 @@ class RobotControlT {
   }
 
   // Batched compute_grf: forces[b] receives foot_forces_grf (3x4, row r / leg l at [r*4+l]).
-  // `dt` is the caller's thread period; it is the horizon step only when use_sim_time is set.
-  // Robot b keeps warm-start slot b from call to call (a change of `count` re-initialises all).
+  // Each robot takes the branch its state.stance_leg_control_type selects (A1RobotControl.cpp:377,
+  // :446): 0 -> the single-step QP balance controller (fresh solve), 1 -> the MPC (this
+  // controller's persistent warm-started solver); states without the field are MPC.  `dt` is the
+  // caller's thread period; it is the horizon step only when use_sim_time is set.  Robot b keeps
+  // MPC warm-start slot b from call to call (a change of `count` re-initialises all); a QP tick
+  // leaves the robot's MPC solver state untouched, as the reference's QP branch leaves the member
+  // solver (it builds a local one, :416).
   template <class State>
   void compute_grf_batch(State* states, int count, double* forces, mpcqp_result* results = nullptr,
                          double dt = 0.0) {
-    if (use_sim_time && !(std::isfinite(dt) && dt > 0.0))
-      throw std::invalid_argument("compute_grf: use_sim_time needs the caller's dt (finite, > 0)");
-    const double hdt = use_sim_time ? dt : mpc_dt;  // A1RobotControl.cpp:462-467
-    recs_.resize((size_t)count * MPCQP_REC_SIZE(N));
+    mpc_idx_.clear();
+    qp_idx_.clear();
+    for (int b = 0; b < count; ++b) {
+      const int ty = control_type_of(states[b]);
+      if (ty == 1) mpc_idx_.push_back(b);
+      else if (ty == 0) qp_idx_.push_back(b);
+      else throw std::invalid_argument("compute_grf: stance_leg_control_type must be 0 (QP) or 1 (MPC)");
+    }
     res_.resize(count);
-    for (int b = 0; b < count; ++b) assemble(states[b], &recs_[(size_t)b * MPCQP_REC_SIZE(N)], hdt);
-    if (warm_start) {
-      ensure_slots(count);
-      throw_on(mpcqp_solve_batch_warm_host(h_, recs_.data(), count, d_state_, res_.data(), nullptr), h_,
-               "mpcqp_solve_batch_warm_host");
-    } else {
-      throw_on(mpcqp_solve_batch_host(h_, recs_.data(), count, res_.data(), nullptr), h_, "mpcqp_solve_batch_host");
+    if (!mpc_idx_.empty()) {
+      if (use_sim_time && !(std::isfinite(dt) && dt > 0.0))
+        throw std::invalid_argument("compute_grf: use_sim_time needs the caller's dt (finite, > 0)");
+      const double hdt = use_sim_time ? dt : mpc_dt;  // A1RobotControl.cpp:462-467
+      const int nm = (int)mpc_idx_.size();
+      recs_.resize((size_t)nm * MPCQP_REC_SIZE(N));
+      sub_res_.resize(nm);
+      for (int i = 0; i < nm; ++i) assemble(states[mpc_idx_[i]], &recs_[(size_t)i * MPCQP_REC_SIZE(N)], hdt);
+      if (warm_start) {
+        ensure_slots(count);
+        if (nm == count) {
+          throw_on(mpcqp_solve_batch_warm_host(h_, recs_.data(), nm, d_state_, sub_res_.data(), nullptr), h_,
+                   "mpcqp_solve_batch_warm_host");
+        } else {  // the MPC robots' slots, gathered and scattered back around the solve
+          DeviceScope ds(device_);
+          const size_t sd = slot_doubles();
+          ensure_gather(nm);
+          for (int i = 0; i < nm; ++i)
+            hip_ok(hipMemcpy(d_gather_ + sd * i, d_state_ + sd * mpc_idx_[i], sizeof(double) * sd,
+                             hipMemcpyDeviceToDevice), "hipMemcpy");
+          throw_on(mpcqp_solve_batch_warm_host(h_, recs_.data(), nm, d_gather_, sub_res_.data(), nullptr), h_,
+                   "mpcqp_solve_batch_warm_host");
+          for (int i = 0; i < nm; ++i)
+            hip_ok(hipMemcpy(d_state_ + sd * mpc_idx_[i], d_gather_ + sd * i, sizeof(double) * sd,
+                             hipMemcpyDeviceToDevice), "hipMemcpy");
+        }
+      } else {
+        throw_on(mpcqp_solve_batch_host(h_, recs_.data(), nm, sub_res_.data(), nullptr), h_, "mpcqp_solve_batch_host");
+      }
+      for (int i = 0; i < nm; ++i) res_[mpc_idx_[i]] = sub_res_[i];
+    }
+    if constexpr (has_control_type<State>::value) {  // (a state type without the field is MPC only)
+     if (!qp_idx_.empty()) {
+      const int nq = (int)qp_idx_.size();
+      bal_recs_.resize((size_t)nq * MPCQP_BAL_SIZE);
+      sub_res_.resize(nq);
+      for (int i = 0; i < nq; ++i) assemble_balance(states[qp_idx_[i]], &bal_recs_[(size_t)i * MPCQP_BAL_SIZE]);
+      throw_on(mpcqp_balance_solve_host(h_, &balance_params, bal_recs_.data(), nq, sub_res_.data()), h_,
+               "mpcqp_balance_solve_host");
+      for (int i = 0; i < nq; ++i) res_[qp_idx_[i]] = sub_res_[i];
+     }
     }
     for (int b = 0; b < count; ++b) {
       for (int l = 0; l < 4; ++l)
@@ -543,9 +737,11 @@ class RobotControlT {
   }
 
   // A1RobotControl::compute_grf(A1CtrlStates& state, double dt) -> Eigen::Matrix<double,3,NUM_LEG>
-  // (A1RobotControl.h:44): single robot, warm-started from this controller's previous call.  Like
-  // the reference, the horizon step is mpc_dt = 0.0025 and `dt` only with use_sim_time (:458-467).
-  // A leg whose solution norm is NaN keeps a zero column (the reference leaves it uninitialised).
+  // (A1RobotControl.h:44): single robot, the branch of state.stance_leg_control_type (0: QP balance,
+  // :377-444; 1: MPC warm-started from this controller's previous MPC call, :446-562).  Like the
+  // reference, the MPC horizon step is mpc_dt = 0.0025 and `dt` only with use_sim_time (:458-467).
+  // A leg whose MPC solution norm is NaN keeps a zero column (the reference leaves it uninitialised).
+  // Terrain adaptation (:335-376) is upstream: pass the adapted root_euler_d.
   template <class State>
   Matrix34 compute_grf(State& state, double dt) {
     double f[12];
@@ -650,12 +846,25 @@ class RobotControlT {
     hip_ok(hipMemset(d_state_, 0, sizeof(double) * slot_doubles() * count), "hipMemset");  // = not initialised
     slots_ = count;
   }
+  void ensure_gather(int count) {
+    if (count <= gather_cap_ && d_gather_) return;
+    DeviceScope ds(device_);
+    if (d_gather_) hip_ok(hipFree(d_gather_), "hipFree");
+    d_gather_ = nullptr;
+    gather_cap_ = 0;
+    hip_ok(hipMalloc(&d_gather_, sizeof(double) * slot_doubles() * count), "hipMalloc");
+    gather_cap_ = count;
+  }
 
   mpcqp_params params_{};
   mpcqp_handle* h_ = nullptr;
   int device_ = 0;
   double* d_state_ = nullptr;
   int slots_ = 0;
+  double* d_gather_ = nullptr;  // mixed-mode batches: the MPC robots' slots, compacted
+  int gather_cap_ = 0;
+  std::vector<int> mpc_idx_, qp_idx_;
+  std::vector<mpcqp_result> sub_res_;
   std::vector<double> recs_;
   std::vector<double> bal_recs_;
   std::vector<mpcqp_result> res_;

@@ -392,6 +392,7 @@ typedef struct {
   int iter, status, rho_updates;
   double pri_res, dua_res, obj_val;
   double mu; /* friction coefficient of the constraint matrix A latched by the last setup */
+  int last_update_mode; /* ws_update's branch: 1 osqp_update_P, 2 OsqpEigen re-init */
 } osqp_ws;
 
 static csc dense_to_csc_upper(const double* M, int n) {
@@ -1248,6 +1249,7 @@ static int ws_update(osqp_ws* w, const double* rec) {
     memcpy(w->P.x, Pn.x, sizeof(double) * Pn.p[n]);
     if (w->st->scaling) scale_data(w);
     fail |= factor_kkt(w);
+    w->last_update_mode = 1;
   } else {
     /* sparsity changed: OsqpEigen re-initializes the solver and restores the unscaled primal
      * and dual variables through osqp_warm_start_x / _y */
@@ -1261,6 +1263,7 @@ static int ws_update(osqp_ws* w, const double* rec) {
     for (int i = 0; i < m; ++i) w->y[i] = w->st->scaling ? w->c * (w->Einv[i] * yu[i]) : yu[i];
     free(xu);
     free(yu);
+    w->last_update_mode = 2;
   }
   csc_free(&Pn);
   /* osqp_update_lin_cost */
@@ -1283,6 +1286,10 @@ struct orc_solver {
   osqp_ws w;
   int initialized;
   mpcqp_params prm;
+  int last_mode; /* branch of the last step: 0 setup (initSolver), 1 osqp_update_P, 2 re-init */
+  /* TEST ONLY (orc_solver_step_image): where the next step copies its scaled data */
+  double *img_D, *img_E, *img_q, *img_c;
+  int32_t* img_mode;
 };
 
 orc_solver* orc_solver_new(const mpcqp_params* prm) {
@@ -1317,8 +1324,18 @@ int32_t orc_solver_step(orc_solver* s, const double* rec, mpcqp_result* res, dou
     ws_alloc(&s->w, &s->prm);
     fail = ws_setup(&s->w, rec);
     s->initialized = 1;
+    s->last_mode = 0;
   } else {
     fail = ws_update(&s->w, rec);
+    s->last_mode = s->w.last_update_mode;
+  }
+  if (s->img_D) { /* TEST ONLY: the scaled data this tick's ADMM starts from */
+    memcpy(s->img_D, s->w.D, sizeof(double) * s->w.n);
+    memcpy(s->img_E, s->w.E, sizeof(double) * s->w.m);
+    memcpy(s->img_q, s->w.q, sizeof(double) * s->w.n);
+    *s->img_c = s->w.c;
+    *s->img_mode = s->last_mode;
+    s->img_D = NULL;
   }
   ws_admm(&s->w, fail, trace, max_trace, n_trace);
   ws_extract(&s->w, rec, res, sol);
@@ -1636,4 +1653,35 @@ int32_t orc_balance_solve_batch(const mpcqp_params* prm, const mpcqp_balance_par
   if (nthreads > 1)
     for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   return MPCQP_OK;
+}
+
+/* TEST ONLY — the scaled problem data an OSQP solve of `rec` starts from (osqp_setup: bound
+ * clipping, scale_data): D [n], E [m], the scaled gradient q~ = c D q [n] and the cost scale c.
+ * Checks the device scale_kernel's image (tests/test_gpu_scale_image.py). */
+int32_t orc_scale_image(const mpcqp_params* prm, const double* rec, double* D, double* E, double* q, double* c) {
+  const int N = prm->horizon;
+  if (N < 1 || record_has_nonfinite(rec, N)) return MPCQP_ERR_INVALID_ARG;
+  osqp_ws w;
+  ws_alloc(&w, prm);
+  ws_setup(&w, rec);
+  memcpy(D, w.D, sizeof(double) * w.n);
+  memcpy(E, w.E, sizeof(double) * w.m);
+  memcpy(q, w.q, sizeof(double) * w.n);
+  *c = w.c;
+  ws_free(&w);
+  return MPCQP_OK;
+}
+
+/* TEST ONLY — orc_solver_step that also reports the scaled data the tick's ADMM starts from (after
+ * initSolver / osqp_update_P / re-init and osqp_update_lin_cost) and the branch taken. */
+int32_t orc_solver_step_image(orc_solver* s, const double* rec, mpcqp_result* res, double* D, double* E, double* q,
+                              double* c, int32_t* mode) {
+  s->img_D = D;
+  s->img_E = E;
+  s->img_q = q;
+  s->img_c = c;
+  s->img_mode = mode;
+  const int32_t rc = orc_solver_step(s, rec, res, NULL, NULL, 0, NULL);
+  s->img_D = NULL;
+  return rc;
 }

@@ -74,6 +74,11 @@ int32_t orc_solve_sequence(const mpcqp_params* prm, const double* recs, int32_t 
  * MPCQP_TQ_SIZE record (include/mpcqp.h), `f_grf` the 12 body-frame GRFs (foot_forces_grf
  * columns, = mpcqp_result.f_body), `counter` the controller's mpc_init_counter (incremented),
  * `tau` the robot's joint_torques (updated in place; NaN entries keep the previous value). */
+/* TEST ONLY: scaled problem data (D, E, q~ = c D q, c) a cold solve / a persistent solver's next
+ * tick starts from; mode = 0 initSolver, 1 osqp_update_P, 2 OsqpEigen re-init. */
+int32_t orc_scale_image(const mpcqp_params* prm, const double* rec, double* D, double* E, double* q, double* c);
+int32_t orc_solver_step_image(orc_solver* s, const double* rec, mpcqp_result* res, double* D, double* E, double* q,
+                              double* c, int32_t* mode);
 void orc_joint_torques(const double* tq, const double* f_grf, int32_t* counter, double* tau);
 
 /* Batch over `nthreads` POSIX threads (static contiguous partition).  sols may be NULL. */

@@ -148,6 +148,11 @@ def lib():
         L.orc_balance_solve_batch.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(BalanceParams), dp,
                                               ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
         L.orc_balance_solve_batch.restype = ctypes.c_int32
+        L.orc_scale_image.argtypes = [ctypes.POINTER(Params), dp, dp, dp, dp, dp]
+        L.orc_scale_image.restype = ctypes.c_int32
+        L.orc_solver_step_image.argtypes = [ctypes.c_void_p, dp, ctypes.c_void_p, dp, dp, dp, dp,
+                                            ctypes.POINTER(ctypes.c_int32)]
+        L.orc_solver_step_image.restype = ctypes.c_int32
         _lib = L
     return _lib
 
@@ -208,6 +213,18 @@ def solve_batch(params, recs, nthreads=1, want_solution=False):
     return (res, sols) if want_solution else res
 
 
+def scale_image(params, rec):
+    """TEST ONLY: OSQP setup's scaled data for rec: {D [12N], E [20N], q (= c D q) [12N], c}."""
+    N = params.horizon
+    out = {"D": np.zeros(12 * N), "E": np.zeros(20 * N), "q": np.zeros(12 * N)}
+    c = np.zeros(1)
+    rec = np.ascontiguousarray(rec, dtype=np.float64)
+    rc = lib().orc_scale_image(ctypes.byref(params), _dp(rec), _dp(out["D"]), _dp(out["E"]), _dp(out["q"]), _dp(c))
+    assert rc == 0
+    out["c"] = float(c[0])
+    return out
+
+
 class WarmSolver:
     """Persistent per-robot OSQP restatement (warm start across control ticks, orc_solver_*)."""
 
@@ -223,6 +240,22 @@ class WarmSolver:
         rc = lib().orc_solver_step(self._s, _dp(rec), ctypes.byref(res), _dp(sol), None, 0, None)
         assert rc == 0
         return np.frombuffer(bytearray(res), dtype=RESULT_DTYPE)[0], sol
+
+    def step_image(self, rec):
+        """step() that also returns the scaled data the tick's ADMM started from:
+        {D, E, q (= c D q), c, mode (0 initSolver, 1 osqp_update_P, 2 re-init)}."""
+        N = self.params.horizon
+        res = Result()
+        img = {"D": np.zeros(12 * N), "E": np.zeros(20 * N), "q": np.zeros(12 * N)}
+        c = ctypes.c_double()
+        mode = ctypes.c_int32()
+        rec = np.ascontiguousarray(rec, dtype=np.float64)
+        rc = lib().orc_solver_step_image(self._s, _dp(rec), ctypes.byref(res), _dp(img["D"]), _dp(img["E"]),
+                                         _dp(img["q"]), ctypes.cast(ctypes.byref(c), ctypes.POINTER(ctypes.c_double)),
+                                         ctypes.byref(mode))
+        assert rc == 0
+        img["c"], img["mode"] = c.value, mode.value
+        return np.frombuffer(bytearray(res), dtype=RESULT_DTYPE)[0], img
 
     def reset(self):
         lib().orc_solver_reset(self._s)

@@ -146,3 +146,65 @@ def test_cpp_warm_ticks_match_oracle_sequence(oracle, tmp_path):
     cold = oracle.solve_batch(oracle.default_params(10), recs_t[1:].reshape(-1, recs_t.shape[-1]), nthreads=4)
     warm = np.array([w for w in warm_iters if w is not None])
     assert warm.mean() < 0.6 * cold["iters"].mean()  # the warm start is really in effect
+
+
+@pytest.mark.gpu
+def test_cpp_compute_grf_dispatches_on_stance_leg_control_type(oracle, tmp_path):
+    """One compute_grf(state, dt) entry point, the branch chosen per tick by
+    state.stance_leg_control_type (A1RobotControl.cpp:377 QP, :446 MPC).  Every robot switches
+    between the branches mid-sequence (per-robot controllers, and one batched controller that gets
+    mixed-mode batches).  QP ticks == the oracle's fresh balance solve of the printed record (bitwise);
+    MPC ticks == the oracle's persistent solver run over that robot's MPC ticks only (the QP branch
+    never touches the member solver, so its warm start carries across the QP ticks)."""
+    exe = os.path.join(REPO, "tests", "cpp", "build", "test_mode_switch_gpu")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(REPO, "tests", "cpp")], check=True)
+    T, B = 16, 4
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=43, gait="trot", swing_ticks=5)
+    rows = np.stack([mpcqp.pack_states(st) for st in ticks])
+    path = tmp_path / "states.bin"
+    np.ascontiguousarray(rows, dtype=np.float64).tofile(path)
+    out = subprocess.run([exe, str(path), str(T), str(B)], check=True, capture_output=True, text=True,
+                         timeout=120).stdout
+    got = {"TICK": {}, "BATCH": {}}
+    grf, balrec = {}, {}
+    for line in out.splitlines():
+        p = line.split()
+        if p[0] in got:
+            got[p[0]][(int(p[1]), int(p[2]))] = (int(p[3]), int(p[4]), int(p[5]), int(p[6]),
+                                                  np.array([float(x) for x in p[7:]]))
+        elif p[0] == "GRF":
+            grf[(int(p[1]), int(p[2]))] = np.array([float(x) for x in p[3:]]).reshape(3, 4)
+        elif p[0] == "BALREC":
+            balrec[(int(p[1]), int(p[2]))] = np.array([float(x) for x in p[3:]])
+    assert "BADTYPE rejected" in out
+
+    def mode(t, b):
+        return 0 if (t + b) % 8 in (3, 4) else 1
+    recs_t = np.stack([mpcqp.assemble_compute_grf(st, 10) for st in ticks])  # [T][B][rec]
+    op = oracle.default_params(10)
+    bp = oracle.default_balance_params()
+    n_qp = n_mpc = 0
+    for b in range(B):
+        mts = [t for t in range(T) if mode(t, b) == 1]
+        ref_m = oracle.solve_sequence(op, np.ascontiguousarray(recs_t[mts, b:b + 1]), nthreads=1)
+        ref_of = {t: ref_m[i][0] for i, t in enumerate(mts)}
+        for t in range(T):
+            for tag in ("TICK", "BATCH"):
+                ty, st, it, ru, u0 = got[tag][(t, b)]
+                assert ty == mode(t, b)
+                if ty == 1:
+                    r = ref_of[t]
+                    assert (st, it) == (int(r["status"]), int(r["iters"])), (tag, t, b)
+                    err = np.max(np.abs(u0 - r["u0"])) / max(np.max(np.abs(r["u0"])), 1.0)
+                    assert err <= 1e-4, (tag, t, b, err)
+                    n_mpc += 1
+                else:
+                    r = oracle.balance_solve_batch(op, bp, balrec[(t, b)][None])[0]
+                    assert (st, it) == (int(r["status"]), int(r["iters"])), (tag, t, b)
+                    np.testing.assert_array_equal(u0, r["u0"])
+                    n_qp += 1
+                if tag == "TICK":
+                    fb = np.array(r["f_body"]).reshape(4, 3).T
+                    assert np.max(np.abs(grf[(t, b)] - fb)) <= 1e-4 * max(np.max(np.abs(fb)), 1.0)
+    assert n_qp > 0 and n_mpc > 0

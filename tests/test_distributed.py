@@ -62,7 +62,7 @@ def test_shard_range_partitions():
             assert max(sizes) - min(sizes) <= 1
 
 
-@pytest.mark.parametrize("world,batch", [(2, 48), (3, 16)])
+@pytest.mark.parametrize("world,batch", [(2, 48), (3, 16), (8, None)])
 def test_bench_launcher_shards_and_gathers(world, batch):
     """bench.py --gpus N as the driver runs it: the parent starts torch.distributed.run as a child
     (no GPU touched), N ranks take contiguous shards of ONE seeded global batch, run the production
@@ -72,9 +72,13 @@ def test_bench_launcher_shards_and_gathers(world, batch):
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(world), "--cpu-stub",
-                          "--steps", "2", "--warmup", "1", "--batch", str(batch)],
-                         capture_output=True, text=True, timeout=300, cwd=repo)
+    argv = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(world), "--cpu-stub",
+            "--steps", "2", "--warmup", "1"]
+    if batch is not None:
+        argv += ["--batch", str(batch)]
+    else:  # the driver's 8-GPU line: no --batch, so the default must be C3 (8192 robots per GPU)
+        batch = 8192
+    out = subprocess.run(argv, capture_output=True, text=True, timeout=600, cwd=repo)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
@@ -83,3 +87,16 @@ def test_bench_launcher_shards_and_gathers(world, batch):
     assert rec["config"]["global_batch"] == world * batch
     assert rec["parity"]["gather_exact"] and rec["parity"]["instances"] == world * batch
     assert rec["value"] > 0 and rec["scaling"] == "weak"
+    assert rec["extras"]["allgather_ms"] >= 0.0
+    if world == 8:
+        assert rec["config"]["global_batch"] == 65536 and rec["config"]["workload"].startswith("C3:")
+
+
+def test_bench_default_batch_is_c2_at_one_gpu_and_c3_shard_above():
+    import bench
+    assert bench.parse_args([]).batch == 4096
+    assert bench.parse_args(["--gpus", "8"]).batch == 8192
+    assert bench.parse_args(["--gpus", "2", "--batch", "100"]).batch == 100
+    assert bench.config_name(10, 4096, 1, "trot", False) == "C2"
+    assert bench.config_name(10, 8192, 8, "trot", False) == "C3"
+    assert bench.config_name(20, 4096, 1, "trot", False) == "C4"

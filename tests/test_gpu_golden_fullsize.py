@@ -103,7 +103,9 @@ def test_c4_fullsize_properties(oracle):
     ref = oracle.solve_batch(oracle.default_params(N), recs[idx], nthreads=8)
     assert np.all(rel_err_u0(got["u0"][idx], ref["u0"]) <= 1e-4)
     np.testing.assert_array_equal(got["status"][idx], ref["status"])
-    assert np.mean(got["iters"][idx] == ref["iters"]) >= 0.95
+    frac = np.mean(got["iters"][idx] == ref["iters"])
+    print(f"full-size sample: iteration-equal fraction {frac:.4f}")
+    assert frac >= 0.99
 
 
 @pytest.mark.parametrize("gait", ["trot", "mixed"])

@@ -5,7 +5,8 @@ The Riccati path runs the same OSQP 0.6 iteration as the dense path; only the re
 instead of an explicit inverse), so rounding differs from the oracle's LDL' solve.  Gates
 (SURVEY §8(c) P1):
   ||du0||_inf / max(||u0||_inf, 1) <= 1e-4, status identical, iteration count within +-25
-  (one termination-check interval) and identical for the large majority of instances.
+  (one termination-check interval) and identical for >= 99 % of the instances (the measured
+  fraction is printed; round 3's bench saw 256 / 256 identical at N = 20).
 """
 import numpy as np
 import pytest
@@ -25,7 +26,7 @@ def _oracle_params(oracle, p):
         eps_abs=p.eps_abs, eps_rel=p.eps_rel, adaptive_rho_interval=p.adaptive_rho_interval)
 
 
-def _check_p1_riccati(oracle, solver, recs, label, min_iter_equal=0.9):
+def _check_p1_riccati(oracle, solver, recs, label, min_iter_equal=0.99):
     op = _oracle_params(oracle, solver.params)
     ref, ref_sol = oracle.solve_batch(op, recs, nthreads=8, want_solution=True)
     got, sol, _ = solve_gpu(solver, recs)
@@ -36,6 +37,7 @@ def _check_p1_riccati(oracle, solver, recs, label, min_iter_equal=0.9):
     np.testing.assert_array_equal(got["status"], ref["status"], err_msg=label)
     di = np.abs(got["iters"].astype(int) - ref["iters"].astype(int))
     assert di.max() <= ITER_TOL, f"{label}: iteration drift {di.max()}"
+    print(f"{label}: iteration-equal fraction {np.mean(di == 0):.4f} of {di.size}")
     assert np.mean(di == 0) >= min_iter_equal, f"{label}: only {np.mean(di == 0):.2f} identical iteration counts"
     fb = np.max(np.abs(got["f_body"] - ref["f_body"]), axis=1) / np.maximum(np.max(np.abs(ref["f_body"]), axis=1), 1)
     assert np.all(fb <= TOL_P1), label

@@ -1,0 +1,122 @@
+"""The product path's own formulation, pinned directly (VERDICT r03 missing 3).
+
+The default solve never materialises ConvexMpc's H: scale_kernel derives H's columns in closed form
+(ConvexMpc.cpp:184-211 structure), the gradient by an adjoint sweep (:215-217), and runs OSQP 0.6's
+scale_data on them (Ruiz passes + cost scaling), handing wave_kernel an image of D, E, q~ and c
+(and, for warm slots, the osqp_update_P / re-init branch).  This test compares that image — read
+back through the debug library's mpcqp_debug_scale_image_device — with the oracle's scaled data
+after osqp_setup (oracle/mpc_oracle.c orc_scale_image) or after a persistent solver's per-tick
+update (orc_solver_step_image), on every golden set and on 256-robot samples of C2 and C5.
+
+Gates: the branch bitwise; D, E within 1e-13 relative, c within 1e-13 relative, q~ within 1e-13 of
+max|q~| (the closed-form columns and the dense B'QB agree to the last bits, not bitwise, so the
+Ruiz norms may differ in the last place)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import mpcqp
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+TOL = 1e-13
+
+
+def _split(img, N):
+    n, m = 12 * N, 20 * N
+    return {"D": img[:, :n], "E": img[:, n:n + m], "q": img[:, n + m:2 * n + m], "qn": img[:, 2 * n + m:3 * n + m],
+            "c": img[:, 3 * n + m], "mode": img[:, 3 * n + m + 1]}
+
+
+def _gpu_image(solver, recs, d_state=None):
+    recs = np.ascontiguousarray(recs, dtype=np.float64)
+    B = recs.shape[0]
+    d_rec = torch.from_numpy(recs).cuda()
+    d_img = torch.full((B, solver.scale_image_size), float("nan"), dtype=torch.float64, device="cuda")
+    solver.scale_image_device(d_rec.data_ptr(), B, d_state.data_ptr() if d_state is not None else 0,
+                              d_img.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return _split(d_img.cpu().numpy(), solver.params.horizon)
+
+
+def _close(a, b, what, scale=None):
+    a, b = np.asarray(a), np.asarray(b)
+    den = np.maximum(np.abs(b), 1e-300) if scale is None else scale
+    err = np.max(np.abs(a - b) / den)
+    assert err <= TOL, f"{what}: {err:.3g}"
+    return err
+
+
+def _check_cold(oracle, recs, N, q=None, r=None, label=""):
+    p = mpcqp.default_params(N, **({} if q is None else {"q_weights": q, "r_weights": r}))
+    op = oracle.default_params(N, q=list(p.q_weights), r=list(p.r_weights))
+    with mpcqp.MpcQpSolver(p, debug=True) as s:
+        g = _gpu_image(s, recs)
+    assert np.all(g["mode"] == 0), label
+    for b in range(recs.shape[0]):
+        ref = oracle.scale_image(op, recs[b])
+        _close(g["D"][b], ref["D"], f"{label}[{b}] D")
+        _close(g["E"][b], ref["E"], f"{label}[{b}] E")
+        _close(g["c"][b], ref["c"], f"{label}[{b}] c")
+        _close(g["q"][b], ref["q"], f"{label}[{b}] q~", scale=max(np.max(np.abs(ref["q"])), 1e-300))
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(HERE, "golden", "*.npz"))),
+                         ids=lambda p: os.path.basename(p)[:-4])
+def test_scale_image_matches_oracle_on_golden_sets(oracle, path):
+    d = np.load(path)
+    if "records" not in d or "q_weights" not in d:
+        pytest.skip("not an MPC golden set")
+    recs = d["records"]
+    N = int(d["horizon"]) if "horizon" in d else (recs.shape[1] - 44) // 25
+    ok = np.all(np.isfinite(recs), axis=1)  # (non-finite records never reach the passes)
+    _check_cold(oracle, recs[ok], N, q=d["q_weights"], r=d["r_weights"], label=os.path.basename(path))
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C5"])
+def test_scale_image_matches_oracle_on_bench_samples(oracle, cfg):
+    gait, mixed = ("trot", False) if cfg == "C2" else ("mixed", True)
+    total = 4096 if cfg == "C2" else 8192
+    st = mpcqp.synthetic_go1(total, seed=(1 if cfg == "C2" else 4) * 1000, gait=gait, mixed_mu=mixed)
+    recs = mpcqp.assemble_compute_grf(st, 10)
+    idx = np.unique(np.linspace(0, total - 1, 256).astype(np.int64))
+    _check_cold(oracle, recs[idx], 10, label=cfg)
+
+
+def test_scale_image_warm_branches_match_oracle(oracle):
+    """Warm slots: per tick the branch (update_P vs re-init) and the scaled data the warm solve starts
+    from (after update_P or re-init, q~ = c (D q) of this tick's gradient: osqp_update_lin_cost, the
+    expression wave_kernel applies to the image's raw gradient)."""
+    T, B, N = 6, 24, 10
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=23, gait="trot", swing_ticks=3)
+    recs_t = np.stack([mpcqp.assemble_compute_grf(s, N) for s in ticks])
+    recs_t[3:, ::3, mpcqp._lib.REC_MU] = 0.5  # a friction change: OsqpEigen re-init for those robots
+    p = mpcqp.default_params(N)
+    op = oracle.default_params(N)
+    ws = [oracle.WarmSolver(op) for _ in range(B)]
+    modes = set()
+    with mpcqp.MpcQpSolver(p, debug=True) as s:
+        d_state = torch.zeros((B, s.warm_state_size), dtype=torch.float64, device="cuda")
+        d_res = torch.zeros((B, mpcqp._lib.RESULT_DOUBLES), dtype=torch.float64, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        for t in range(T):
+            g = _gpu_image(s, recs_t[t], d_state.clone())  # (the pass records H's pattern: a copy)
+            d_rec = torch.from_numpy(np.ascontiguousarray(recs_t[t])).cuda()
+            s.solve_warm_device(d_rec.data_ptr(), B, d_state.data_ptr(), d_res.data_ptr(), 0, stream)
+            torch.cuda.synchronize()
+            for b in range(B):
+                _, ref = ws[b].step_image(recs_t[t, b])
+                assert int(g["mode"][b]) == ref["mode"], (t, b)
+                modes.add(ref["mode"])
+                _close(g["D"][b], ref["D"], f"tick {t} robot {b} D")
+                _close(g["E"][b], ref["E"], f"tick {t} robot {b} E")
+                _close(g["c"][b], ref["c"], f"tick {t} robot {b} c")
+                q = (g["qn"][b] * g["D"][b]) * g["c"][b] if ref["mode"] != 0 else g["q"][b]
+                _close(q, ref["q"], f"tick {t} robot {b} q~", scale=max(np.max(np.abs(ref["q"])), 1e-300))
+    for w in ws:
+        w.close()
+    assert modes == {0, 1, 2}, modes

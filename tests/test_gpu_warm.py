@@ -2,7 +2,8 @@
 solver (oracle/mpc_oracle.c orc_solver_step: OsqpEigen 0.6.3 initSolver on the first tick, then
 updateHessianMatrix / updateGradient / updateLowerBound / updateUpperBound and a warm-started
 solve; A1RobotControl.cpp:522-540).  Gates per tick: SURVEY §8(c) P1 (u0 within 1e-4 relative,
-status identical, iterations within one check interval)."""
+status identical, iterations within one check interval and identical for >= 99 % of the robots of
+every tick; the measured fraction is printed)."""
 import numpy as np
 import pytest
 import torch
@@ -34,7 +35,7 @@ def _gpu_sequence(params, recs_t):
     return out
 
 
-def _check(got, ref, label, min_iter_equal=0.9):
+def _check(got, ref, label, min_iter_equal=0.99):
     for t in range(got.shape[0]):
         np.testing.assert_array_equal(got[t]["status"], ref[t]["status"], err_msg=f"{label} tick {t}")
         ok = ref[t]["status"] != mpcqp._lib.STATUS_NAN_INPUT  # those carry NaN forces on both sides
@@ -42,6 +43,7 @@ def _check(got, ref, label, min_iter_equal=0.9):
         assert np.all(err <= 1e-4), f"{label} tick {t}: worst {err.max():.3g}"
         di = np.abs(got[t]["iters"].astype(int) - ref[t]["iters"].astype(int))
         assert di.max() <= 25, f"{label} tick {t}: iteration drift {di.max()}"
+        print(f"{label} tick {t}: iteration-equal fraction {np.mean(di == 0):.4f}")
         assert np.mean(di == 0) >= min_iter_equal, f"{label} tick {t}: {np.mean(di == 0):.2f} equal"
 
 
@@ -135,7 +137,7 @@ def test_python_robot_control_is_warm_and_mutates_state(oracle):
             f = ctrl.compute_grf(st, dt=0.002)
             got = ctrl.last_results
             np.testing.assert_array_equal(got["status"], ref[t]["status"])
-            assert np.mean(got["iters"] == ref[t]["iters"]) >= 0.9
+            assert np.mean(got["iters"] == ref[t]["iters"]) >= 0.99
             assert np.all(rel_err_u0(got["u0"], ref[t]["u0"]) <= 1e-4)
             np.testing.assert_allclose(f, ref[t]["f_body"].reshape(B, 4, 3).transpose(0, 2, 1), atol=1e-4 * 200)
             np.testing.assert_array_equal(st.mpc_states, recs_t[t][:, :13])
