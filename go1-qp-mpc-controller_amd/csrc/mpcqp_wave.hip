@@ -410,7 +410,7 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
                                            mpcqp_result* __restrict__ results, double* __restrict__ solution,
                                            double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
                                            const double* __restrict__ img, const mpcqp_params& p,
-                                           int* __restrict__ fb) {
+                                           int* __restrict__ fb, double* __restrict__ spill) {
   using C = Cfg<N>;
   using WL = WarmLayout<N>;
   constexpr int n = C::n, m = C::m, R = C::R;
@@ -450,12 +450,10 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
   wave_sync();
   WV_MARK(1);
   const double* rec = HS.rec;
-  // Record values used after the setup image is recycled (the LDS union is rewritten by the
-  // factorization) are pinned into registers: keep() hides their origin, so the compiler cannot
-  // rematerialize them by reloading the (by then overwritten) LDS words.
-  double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS];
-  keep(dt);
-  keep(mass);
+  // (record values used after the setup image is recycled are plain register copies: every LDS
+  // store of the union aliases them under -fno-strict-aliasing, so no reload can be hoisted past
+  // the factorization's stores — see DESIGN §5, "LDS unions and aliasing")
+  const double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS], mu_rec = rec[MPCQP_REC_MU];
   Adisc A;
   {
     const double yaw = rec[MPCQP_REC_EULER + 2];
@@ -466,11 +464,8 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
   const double dtm = (1.0 / mass) * dt;
   // what the solve needs from the record after the setup image is recycled (root_rot_mat is read
   // again from HBM by the epilogue)
-  double cont = rec[MPCQP_REC_CONTACTS + leg] != 0.0 ? 1.0 : 0.0;
-  double fzmin = rec[MPCQP_REC_FZMIN], fzmax = rec[MPCQP_REC_FZMAX];
-  keep(cont);
-  keep(fzmin);
-  keep(fzmax);
+  const double cont = rec[MPCQP_REC_CONTACTS + leg] != 0.0 ? 1.0 : 0.0;
+  const double fzmin = rec[MPCQP_REC_FZMIN], fzmax = rec[MPCQP_REC_FZMAX];
 
   // ---- 1. B_d(k) rows 6-8 (calculate_B_mat_c, Utils.cpp:35-41), gradient adjoint --------------------
   {
@@ -518,9 +513,8 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
       if (which == 0) return k5 < 4 ? (ws[WL::AK + ri] * ei) * (1. / ws[WL::D + 3 * f + (k5 >> 1)]) : 0.0;
       return (ws[WL::AK + m + ri] * ei) * (1. / ws[WL::D + 3 * f + 2]);
     }
-    const double mu = rec[MPCQP_REC_MU];
     if (which == 0) return k5 < 4 ? 1.0 : 0.0;
-    return k5 < 4 ? ((k5 & 1) ? -mu : mu) : 1.0;
+    return k5 < 4 ? ((k5 & 1) ? -mu_rec : mu_rec) : 1.0;
   };
   wave_sync();
   const double cost_c = c_s, cinv = 1. / c_s;
@@ -715,6 +709,7 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
   double rho = rho0, rinv = 1. / rho0, pri_res = 0.0, dua_res = 0.0;
   int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
   bool handoff = false;  // KS = 1: this robot goes to the Riccati fallback (see schur_factor)
+  double obj_sum = 0.0;  // 1/2 x'P~x + q~'x of the final iterate (scaled), set when the loop ends
   bool need_factor = true;
   int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
   for (int iter = 1; iter <= p.max_iter; ++iter) {
@@ -1029,7 +1024,10 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
     if (tm_ck) WV_MARK(48);
     if (need_info) {
       // ---- update_info / check_termination / adapt_rho (osqp.c, auxil.c) ----
-      if constexpr (KS == 1) px_of(X, PX);
+      // KS = 1: P~x of this iterate, local to the check (not carried through the loop)
+      double PXl[R];
+      double (&PXc)[R] = KS == 1 ? PXl : PX;
+      if constexpr (KS == 1) px_of(X, PXc);
       if (tm_ck) WV_MARK(50);
       // The norms of update_info / check_termination / compute_rho_estimate, and the first-level
       // quantities of both infeasibility tests (||E dy||, the support term of dy, ||D dx||, q'dx:
@@ -1068,11 +1066,11 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
           mx[3] = nmax(mx[3], nmax(nmax(dabs(Z[r]), dabs(Z4[r])), nmax(dabs(ax), dabs(ax4))));
         }
         if (vvr[r]) {
-          const double d = (Qv[r] + 1.0 * PX[r]) + 1.0 * aty;
+          const double d = (Qv[r] + 1.0 * PXc[r]) + 1.0 * aty;
           mx[4] = nmax(mx[4], dabs(DI[r] * d));
           mx[5] = nmax(mx[5], dabs(d));
-          mx[6] = nmax(mx[6], nmax(nmax(dabs(DI[r] * Qv[r]), dabs(DI[r] * aty)), dabs(DI[r] * PX[r])));
-          mx[7] = nmax(mx[7], nmax(nmax(dabs(Qv[r]), dabs(aty)), dabs(PX[r])));
+          mx[6] = nmax(mx[6], nmax(nmax(dabs(DI[r] * Qv[r]), dabs(DI[r] * aty)), dabs(DI[r] * PXc[r])));
+          mx[7] = nmax(mx[7], nmax(nmax(dabs(Qv[r]), dabs(aty)), dabs(PXc[r])));
         }
         // is_primal_infeasible: ||E dy||_inf and u'max(dy, 0) + l'min(dy, 0) of the projected dy
         const double lo = lo03(evr), hi = hi03(evr);
@@ -1185,7 +1183,14 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
       }
 #endif
       ntrace += is_check ? 1 : 0;
-      if (done) break;
+      if (done) {
+        // the objective of the final iterate (every exit of the loop is a need_info iteration)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (vvr[r]) obj_sum += 0.5 * X[r] * PXc[r] + Qv[r] * X[r];
+        obj_sum = wave_sum(obj_sum);
+        break;
+      }
       if (refactor) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -1218,10 +1223,8 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
     if (t == 0) {
       ws[WL::FLAG] = 1.0;
       ws[WL::RHO] = rho;
-      // c and mu reloaded from HBM here rather than carried through the loop (values live across
-      // the whole solve are the ones the register allocator parks in AGPRs / scratch)
-      ws[WL::C] = img_at(SI::CS);
-      ws[WL::MU] = ((const volatile double*)(recs + (size_t)inst * C::REC))[MPCQP_REC_MU];
+      ws[WL::C] = cost_c;
+      ws[WL::MU] = mu_rec;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -1254,12 +1257,7 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
                        status != MPCQP_STATUS_PRIMAL_INFEASIBLE_INACCURATE &&
                        status != MPCQP_STATUS_DUAL_INFEASIBLE &&
                        status != MPCQP_STATUS_DUAL_INFEASIBLE_INACCURATE && status != MPCQP_STATUS_NON_CVX;
-  // (the loop always ends on a need_info iteration: P~x is that of the final x)
-  double ob = 0.0;
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-    if (vvr[r]) ob += 0.5 * X[r] * PX[r] + Qv[r] * X[r];
-  ob = wave_sum(ob);
+  const double ob = obj_sum;
   double xs0 = 0.0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -1310,11 +1308,11 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                                                      double* __restrict__ solution, double* __restrict__ trace,
                                                      int trace_cap, double* __restrict__ wstate,
                                                      const double* __restrict__ img, mpcqp_params p,
-                                                     int* __restrict__ fb) {
+                                                     int* __restrict__ fb, double* __restrict__ spill) {
   __shared__ WSmem<N, KS> sm;
   const int inst = blockIdx.x;
   if (inst >= batch) return;
-  wave_solve<N, KS>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb);
+  wave_solve<N, KS>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb, spill);
 }
 
 // The robots wave_kernel<N, 1> handed over (fb[0] of them at fb[1..]), by the Riccati form; a
@@ -1330,7 +1328,7 @@ __global__ __launch_bounds__(NT, 1) void wave_fallback_kernel(const double* __re
   __shared__ WSmem<N, 0> sm;
   const int cnt = fb[0];
   for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
-    wave_solve<N, 0>(fb[1 + j], sm, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr);
+    wave_solve<N, 0>(fb[1 + j], sm, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr, nullptr);
     wave_sync();
   }
 }
@@ -1364,7 +1362,7 @@ static bool schur_ok(const mpcqp_params& p) {
 }
 template <int N>
 static hipError_t launch_wave(const LaunchArgs& a) {
-  if (!a.fallback) return hipErrorInvalidValue;
+  if (!a.fallback || (N <= 10 && !a.spill)) return hipErrorInvalidValue;
   hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
                      a.recs, a.batch, a.wstate, a.work, a.p, a.fallback);
   hipError_t e = hipGetLastError();
@@ -1372,7 +1370,8 @@ static hipError_t launch_wave(const LaunchArgs& a) {
   if constexpr (N <= 10) {
     if (schur_ok(a.p)) {
       hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs,
-                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
+                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback,
+                         a.spill);
       e = hipGetLastError();
       if (e != hipSuccess) return e;
       // the robots with (nearly) singular G_k, if any (an empty list costs one short launch)
@@ -1383,7 +1382,7 @@ static hipError_t launch_wave(const LaunchArgs& a) {
     }
   }
   hipLaunchKernelGGL((wv::wave_kernel<N, 0>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs, a.batch,
-                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
+                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback, nullptr);
   return hipGetLastError();
 }
 template <int N>
