@@ -167,13 +167,11 @@ __device__ __forceinline__ double alpha_jl(int N, int j, int l) {
 // ---- factorization (once per rho) ----------------------------------------------------------------
 // Inputs: sc.Rt (R'_k foot blocks, written by the caller's variable lanes), sm.Bw.  Outputs: Q and
 // B in LDS and, per lane, RI[r][3] (row a of R'^-1 of its foot, variable role).
-// degen (wave-uniform): set when a Cholesky pivot of some step's G_k is not above SCHUR_PIVOT_TOL
-// times its diagonal entry (rank-deficient B6_k: collinear / coincident feet); the caller then
-// abandons the Schur form for this robot.  On the Go1 workloads the smallest ratio is ~1e-3 (any rho).
-constexpr double SCHUR_PIVOT_TOL = 1e-7;
+// (G_k is positive definite for the robots that reach it: scale_kernel screens out rank-deficient
+// B6_k, whose robots the Riccati form solves)
 template <int N, int R, class SM, class Mark>
 __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp_params& p, const Adisc& A, double cost_c,
-                             double dtm, double (&RI)[R][3], Mark&& mark, bool& degen) {
+                             double dtm, double (&RI)[R][3], Mark&& mark) {
   constexpr int QS = SchurCfg<N>::QS;
   constexpr int NI = SchurCfg<N>::NI;
   auto& sc = F.s;
@@ -248,14 +246,11 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   for (int r2 = 0; r2 < 6; ++r2)
 #pragma unroll
     for (int c2 = 0; c2 < 6; ++c2) L[r2][c2] = 0.0;
-  bool bad = false;
 #pragma unroll
   for (int cc = 0; cc < 6; ++cc) {
-    const double g0 = sc.G[k][6 * cc + cc];
-    double s = g0;
+    double s = sc.G[k][6 * cc + cc];
 #pragma unroll
     for (int e = 0; e < cc; ++e) s -= L[cc][e] * L[cc][e];
-    bad |= !(s > SCHUR_PIVOT_TOL * g0);  // (also NaN)
     const double dg = sqrt(s), dinv = recip(dg);
     L[cc][cc] = dg;
     Ldi[cc] = dinv;
@@ -281,7 +276,6 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
       Li[r2][cc] = v * Ldi[r2];
     }
   }
-  degen = __ballot(bad) != 0;  // (wave-uniform at once: no per-lane flag live through the sweep)
   // the lane's column c of L and row c of Li (c is per lane: selects, not register indexing)
   double Lc[6], lic[6];
 #pragma unroll

@@ -91,6 +91,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   const double dtm = (1.0 / mass) * dt;
   // B_d(k) rows 6-8 (calculate_B_mat_c, Utils.cpp:35-41), gradient adjoint (ConvexMpc.cpp:215-217)
   {
+    int degen = 0;
     double Iwinv[9];
     iw_inverse(rec, Iwinv);
     for (int e = t; e < N * 36; e += NTS) {
@@ -143,8 +144,65 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
         }
         wave_sync();
       }
+    } else if (t < 64 + N) {
+      // Degenerate-foot screen for the Schur form (wave_kernel KS = 1), by wave 1 while wave 0 runs
+      // the sweep: per step k the Cholesky pivots of the Gram matrix B6_k B6_k' (B6 = rows 6-11 of
+      // B_d(k): I_w^-1 [r_l]x dt and dt/m sums) relative to its diagonal.  Collinear feet give rank
+      // 5, coincident feet rank 3; a pivot ratio below SCHUR_GRAM_TOL sends the robot to the Riccati
+      // form.  (Go1 workloads: smallest ratio ~0.12; with R'^-1 between B6 and B6' (spread <= ~1e3)
+      // the Schur form then factors G_k with pivot ratios above ~1e-9.)
+      const int k = t - 64;
+      double bw[3][ND];
+#pragma unroll
+      for (int lg = 0; lg < 4; ++lg) {
+        const double* fp = rec + MPCQP_REC_FEET(N) + 12 * k + 3 * lg;
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {  // (I_w^-1 [r]x)[rr][c3] = sum_e Iwinv[rr][e] skew[e][c3]
+          const double i0 = Iwinv[3 * rr], i1 = Iwinv[3 * rr + 1], i2 = Iwinv[3 * rr + 2];
+          bw[rr][3 * lg + 0] = (i1 * fp[2] - i2 * fp[1]) * dt;
+          bw[rr][3 * lg + 1] = (i2 * fp[0] - i0 * fp[2]) * dt;
+          bw[rr][3 * lg + 2] = (i0 * fp[1] - i1 * fp[0]) * dt;
+        }
+      }
+      double G[21];  // lower triangle, row-major packed; Cholesky in place
+      auto gi = [](int r1, int r2) { return r1 * (r1 + 1) / 2 + r2; };
+#pragma unroll
+      for (int r1 = 0; r1 < 6; ++r1)
+#pragma unroll
+        for (int r2 = 0; r2 <= r1; ++r2) {
+          double g = 0.0;
+          if (r1 < 3) {
+#pragma unroll
+            for (int b = 0; b < ND; ++b) g += bw[r1][b] * bw[r2][b];
+          } else if (r2 < 3) {
+#pragma unroll
+            for (int l = 0; l < 4; ++l) g += bw[r2][3 * l + (r1 - 3)] * dtm;
+          } else {
+            g = r1 == r2 ? 4.0 * dtm * dtm : 0.0;
+          }
+          G[gi(r1, r2)] = g;
+        }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const double d0 = G[gi(c, c)];
+        double sc = d0;
+#pragma unroll
+        for (int e = 0; e < c; ++e) sc -= G[gi(c, e)] * G[gi(c, e)];
+        degen |= !(sc > SCHUR_GRAM_TOL * d0);
+        const double dg = sqrt(dmax(sc, 0.0)), di = dg > 0.0 ? 1.0 / dg : 0.0;
+        G[gi(c, c)] = dg;
+#pragma unroll
+        for (int r1 = c + 1; r1 < 6; ++r1) {
+          double v = G[gi(r1, c)];
+#pragma unroll
+          for (int e = 0; e < c; ++e) v -= G[gi(r1, e)] * G[gi(c, e)];
+          G[gi(r1, c)] = v * di;
+        }
+      }
     }
-    __syncthreads();
+    // (written at once: nothing of the screen stays live through the Ruiz passes)
+    const int any_degen = __syncthreads_or(degen);
+    if (t == 0) img[(size_t)inst * ScaleImg<N>::SIZE + ScaleImg<N>::DEGEN] = any_degen ? 1.0 : 0.0;
   }
   // thread t: column j0 = t / 4, blocks jb .. jb+BPT-1 of it (the column's four threads are a quad)
   constexpr int BPT = SC::BPT;
@@ -494,6 +552,16 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
   const double* im = img + (size_t)inst * SI::SIZE;
   const double c_s = im[SI::CS];
   const int mode = (int)im[SI::MODE];  // 0 cold, 1 osqp_update_P, 2 OsqpEigen re-init
+  if (KS == 1 && im[SI::DEGEN] != 0.0) {
+    // rank-deficient B6_k (collinear / coincident feet, scale_kernel's screen): G_k would be
+    // singular.  The reference QP is still strictly convex (R > 0); the Riccati form (KS = 0,
+    // wave_fallback_kernel) solves this robot.  Nothing of it has been written yet.
+    if (t == 0) {
+      const int j = atomicAdd(fb, 1);
+      fb[1 + j] = inst;
+    }
+    return;
+  }
   for (int j = t; j < n; j += NT) {
     HS.D[j] = im[SI::D + j];
     HS.q[j] = im[SI::Q + j];
@@ -708,7 +776,6 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
   };
   double rho = rho0, rinv = 1. / rho0, pri_res = 0.0, dua_res = 0.0;
   int status = MPCQP_STATUS_UNSOLVED, iters = 0, rho_updates = 0, ntrace = 0;
-  bool handoff = false;  // KS = 1: this robot goes to the Riccati fallback (see schur_factor)
   double obj_sum = 0.0;  // 1/2 x'P~x + q~'x of the final iterate (scaled), set when the loop ends
   bool need_factor = true;
   int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
@@ -756,16 +823,8 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
       wave_sync();
       if constexpr (KS == 0) factorize_mfma<N>(sm, p, A, cost_c, dtm, Q2J);
       else {
-        bool degen = false;
         schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI,
-                           [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; }, degen);
-        // G_k = B6_k R'^-1 B6_k' (nearly) singular: collinear or coincident feet make B6_k rank
-        // deficient (the reference QP is still strictly convex through R).  The Riccati form
-        // (KS = 0) solves this robot instead; nothing of it has been written yet.
-        if (degen) {
-          handoff = true;
-          break;
-        }
+                           [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; });
       }
       wave_sync();
 #ifdef MPCQP_REPEAT_FACTOR
@@ -1212,13 +1271,6 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
   }
 
   WV_MARK(20);
-  if (handoff) {  // nothing of this robot has been written: the fallback kernel solves it
-    if (t == 0) {
-      const int j = atomicAdd(fb, 1);
-      fb[1 + j] = inst;
-    }
-    return;
-  }
   if (ws) {  // the solver persists: scaling, scaled data, iterates and rho for the next tick
     if (t == 0) {
       ws[WL::FLAG] = 1.0;

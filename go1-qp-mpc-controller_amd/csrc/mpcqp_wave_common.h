@@ -533,10 +533,13 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
 // wave_kernel reads in place of its own setup.  H's columns come from the same closed
 // form as before (see gen_col), so every norm is binary64; only the order of the cost-scaling sum
 // over columns differs from the single-wave version (a different but equally exact summation).
+// B6_k Gram pivot ratio below which a robot is handed to the Riccati form (scale_kernel's screen)
+constexpr double SCHUR_GRAM_TOL = 1e-6;
 template <int N>
 struct ScaleImg {
   static constexpr int n = ND * N, m = CD * N;
-  static constexpr int D = 0, E = D + n, Q = E + m, QN = Q + n, CS = QN + n, MODE = CS + 1, SIZE = MODE + 1;
+  static constexpr int D = 0, E = D + n, Q = E + m, QN = Q + n, CS = QN + n, MODE = CS + 1, DEGEN = MODE + 1,
+                       SIZE = DEGEN + 1;
   static_assert(SIZE == scale_image_doubles(N), "scale image layout");
 };
 

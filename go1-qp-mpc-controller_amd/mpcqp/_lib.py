@@ -158,10 +158,11 @@ def load(debug=False):
     L.mpcqp_debug_set_solver.restype = i32
     L.mpcqp_debug_wave_selftest.argtypes = [vp, vp]
     L.mpcqp_debug_wave_selftest.restype = i32
-    L.mpcqp_debug_scale_image_doubles.argtypes = [i32]
-    L.mpcqp_debug_scale_image_doubles.restype = i32
-    L.mpcqp_debug_scale_image_device.argtypes = [vp, vp, i32, vp, vp, vp]
-    L.mpcqp_debug_scale_image_device.restype = i32
+    if hasattr(L, "mpcqp_debug_scale_image_device"):  # (absent from older experiment builds)
+        L.mpcqp_debug_scale_image_doubles.argtypes = [i32]
+        L.mpcqp_debug_scale_image_doubles.restype = i32
+        L.mpcqp_debug_scale_image_device.argtypes = [vp, vp, i32, vp, vp, vp]
+        L.mpcqp_debug_scale_image_device.restype = i32
     L.mpcqp_joint_torques_device.argtypes = [vp, vp, i32, vp, vp, vp]
     L.mpcqp_joint_torques_device.restype = i32
     L.mpcqp_warm_state_size.argtypes = [i32]

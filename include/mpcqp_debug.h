@@ -39,7 +39,8 @@ int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path);
  * warm slots the update_P / re-init branch): per robot mpcqp_debug_scale_image_doubles(N) doubles
  *   [0, 12N) D, [12N, 32N) E, [32N, 44N) q~ (cold / re-init: c D q; update_P: the previous tick's
  *   scaled gradient re-scaled), [44N, 56N) this tick's raw gradient q (warm slots), [56N] c,
- *   [56N + 1] branch (0 cold, 1 osqp_update_P, 2 OsqpEigen re-init).
+ *   [56N + 1] branch (0 cold, 1 osqp_update_P, 2 OsqpEigen re-init), [56N + 2] 1 if some step's
+ *   B6_k is rank deficient (collinear / coincident feet: the robot is solved by the Riccati form).
  * d_state: warm slots as for mpcqp_solve_batch_warm_device, or NULL (cold).  Note that the pass
  * records H's zero pattern into the slots (as the solve's own pass does): run it on a copy.
  * libmpcqp_debug.so only (the product library returns MPCQP_ERR_INVALID_ARG). */

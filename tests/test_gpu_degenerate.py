@@ -1,8 +1,8 @@
 """Degenerate foot geometry (mpcqp_schur.h): the Schur-form KKT solve factors
 G_k = B6_k R'^-1 B6_k', which is singular when the feet are coincident (e.g. all foot_pos_abs zero
 before the first kinematics update) or collinear — B6_k then has rank 3 or 5.  The reference QP is
-still strictly convex (R > 0) and OSQP solves it; the engine hands such robots to the Riccati form
-(wave_fallback_kernel).  Gates: status and iteration count identical to the oracle, u0 within 1e-4
+still strictly convex (R > 0) and OSQP solves it; scale_kernel screens every step's B6_k (Gram
+pivot ratio) and the engine hands such robots to the Riccati form (wave_fallback_kernel).  Gates: status and iteration count identical to the oracle, u0 within 1e-4
 relative, every force finite, and the non-degenerate robots of a mixed batch bit-identical to
 solving them without the degenerate ones."""
 import numpy as np
@@ -49,6 +49,20 @@ def test_degenerate_feet_match_oracle(oracle, gait):
     np.testing.assert_array_equal(got["status"], ref["status"])
     np.testing.assert_array_equal(got["iters"], ref["iters"])
     assert np.all(rel_err_u0(got["u0"], ref["u0"]) <= 1e-4)
+
+
+def test_degenerate_flag_in_scale_image(oracle):
+    """The screen flags exactly the rank-deficient robots (debug library image, slot 56N + 2)."""
+    st = mpcqp.synthetic_go1(16, seed=912, gait="trot")
+    recs = mpcqp.assemble_compute_grf(st, N)
+    recs[::2] = _degenerate(recs[::2])
+    with mpcqp.MpcQpSolver(mpcqp.default_params(N), debug=True) as s:
+        d_rec = torch.from_numpy(recs).cuda()
+        d_img = torch.zeros((16, s.scale_image_size), dtype=torch.float64, device="cuda")
+        s.scale_image_device(d_rec.data_ptr(), 16, 0, d_img.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        flag = d_img.cpu().numpy()[:, 56 * N + 2]
+    np.testing.assert_array_equal(flag, np.tile([1.0, 0.0], 8))
 
 
 def test_degenerate_robots_in_a_large_batch(oracle):

@@ -29,7 +29,7 @@ TOL = 1e-13
 def _split(img, N):
     n, m = 12 * N, 20 * N
     return {"D": img[:, :n], "E": img[:, n:n + m], "q": img[:, n + m:2 * n + m], "qn": img[:, 2 * n + m:3 * n + m],
-            "c": img[:, 3 * n + m], "mode": img[:, 3 * n + m + 1]}
+            "c": img[:, 3 * n + m], "mode": img[:, 3 * n + m + 1], "degen": img[:, 3 * n + m + 2]}
 
 
 def _gpu_image(solver, recs, d_state=None):
@@ -57,6 +57,7 @@ def _check_cold(oracle, recs, N, q=None, r=None, label=""):
     with mpcqp.MpcQpSolver(p, debug=True) as s:
         g = _gpu_image(s, recs)
     assert np.all(g["mode"] == 0), label
+    assert np.all(g["degen"] == 0), label  # (no golden / bench robot has rank-deficient feet)
     for b in range(recs.shape[0]):
         ref = oracle.scale_image(op, recs[b])
         _close(g["D"][b], ref["D"], f"{label}[{b}] D")
