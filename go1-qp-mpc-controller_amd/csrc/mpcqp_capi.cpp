@@ -23,7 +23,6 @@ struct mpcqp_handle {
   size_t work_cap = 0;       // instances the workspace can hold
   size_t work_per = 0;       // doubles per instance the workspace was sized for
   int* fb = nullptr;         // wave path: Schur -> Riccati fallback list [work_cap + 1] ints
-  double* spill = nullptr;   // wave path: the Schur-form kernel's spill rows [work_cap][wave_spill_doubles]
   int path = 0;              // 0 auto (= 3), 3 Riccati wave; debug library only: 1 dense K^-1, 2 Riccati workgroup
   // host wrapper: device buffers, a private stream and two pinned staging chunks
   hipStream_t hstream = nullptr;
@@ -106,17 +105,13 @@ hipError_t ensure_workspace(mpcqp_handle* h, int32_t batch, void* stream) {
   hipError_t e = hipStreamSynchronize((hipStream_t)stream);
   if (e == hipSuccess) e = hipFree(h->work);
   if (e == hipSuccess) e = hipFree(h->fb);
-  if (e == hipSuccess) e = hipFree(h->spill);
   h->work = nullptr;
   h->fb = nullptr;
-  h->spill = nullptr;
   const size_t cap = (size_t)batch > h->work_cap ? (size_t)batch : h->work_cap;
   h->work_cap = 0;
   h->work_per = 0;
   if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * per * cap);
   if (e == hipSuccess) e = hipMalloc(&h->fb, sizeof(int) * (cap + 1));
-  const size_t sp = (size_t)mpcqp::wave_spill_doubles(h->p.horizon);
-  if (e == hipSuccess && sp) e = hipMalloc(&h->spill, sizeof(double) * sp * cap);
   if (e == hipSuccess) {
     h->work_cap = cap;
     h->work_per = per;
@@ -257,7 +252,6 @@ int32_t mpcqp_destroy(mpcqp_handle* h) {
   DeviceGuard dg(h->device);
   (void)hipFree(h->work);
   (void)hipFree(h->fb);
-  (void)hipFree(h->spill);
   (void)hipFree(h->d_recs);
   (void)hipFree(h->d_res);
   (void)hipFree(h->d_sol);
@@ -295,7 +289,6 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   a.trace_cap = d_trace ? trace_cap : 0;
   a.wstate = d_state;
   a.fallback = h->fb;
-  a.spill = h->spill;
   a.grid = batch;
   a.stream = stream;
   a.p = h->p;

@@ -19,7 +19,6 @@ struct LaunchArgs {
   int trace_cap;
   double* wstate;  // warm-start slots [batch][warm_state_doubles(N)] (wave path) or nullptr
   int* fallback;   // wave path: [batch + 1] ints, the Schur -> Riccati fallback list (handle-owned)
-  double* spill;   // wave path, N <= 10: [batch][wave_spill_doubles(N)] (handle-owned)
   int grid;
   void* stream;
   mpcqp_params p;
@@ -57,9 +56,6 @@ __host__ __device__ constexpr int warm_state_doubles(int N) {
 
 // doubles per robot of the scaling image scale_kernel hands to wave_kernel (mpcqp_wave.hip ScaleImg)
 __host__ __device__ constexpr int scale_image_doubles(int N) { return 3 * 12 * N + 20 * N + 3; }
-// doubles per robot of the Schur-form wave kernel's spill rows (the ADMM iterates x, z, y, z4, y4 of
-// each register round, one row of 64 lanes each, stored around a factorization); 0 when N > 10
-__host__ __device__ constexpr int wave_spill_doubles(int N) { return N <= 10 ? 5 * ((N + 3) / 4) * 64 : 0; }
 
 // Downstream torque map (mpcqp_torque.hip)
 hipError_t launch_torques(const double* recs, const mpcqp_result* grf, int batch, int* counter, double* tau,

@@ -468,7 +468,7 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
                                            mpcqp_result* __restrict__ results, double* __restrict__ solution,
                                            double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
                                            const double* __restrict__ img, const mpcqp_params& p,
-                                           int* __restrict__ fb, double* __restrict__ spill) {
+                                           int* __restrict__ fb) {
   using C = Cfg<N>;
   using WL = WarmLayout<N>;
   constexpr int n = C::n, m = C::m, R = C::R;
@@ -1360,11 +1360,11 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                                                      double* __restrict__ solution, double* __restrict__ trace,
                                                      int trace_cap, double* __restrict__ wstate,
                                                      const double* __restrict__ img, mpcqp_params p,
-                                                     int* __restrict__ fb, double* __restrict__ spill) {
+                                                     int* __restrict__ fb) {
   __shared__ WSmem<N, KS> sm;
   const int inst = blockIdx.x;
   if (inst >= batch) return;
-  wave_solve<N, KS>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb, spill);
+  wave_solve<N, KS>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb);
 }
 
 // The robots wave_kernel<N, 1> handed over (fb[0] of them at fb[1..]), by the Riccati form; a
@@ -1380,7 +1380,7 @@ __global__ __launch_bounds__(NT, 1) void wave_fallback_kernel(const double* __re
   __shared__ WSmem<N, 0> sm;
   const int cnt = fb[0];
   for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
-    wave_solve<N, 0>(fb[1 + j], sm, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr, nullptr);
+    wave_solve<N, 0>(fb[1 + j], sm, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr);
     wave_sync();
   }
 }
@@ -1414,7 +1414,7 @@ static bool schur_ok(const mpcqp_params& p) {
 }
 template <int N>
 static hipError_t launch_wave(const LaunchArgs& a) {
-  if (!a.fallback || (N <= 10 && !a.spill)) return hipErrorInvalidValue;
+  if (!a.fallback) return hipErrorInvalidValue;
   hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
                      a.recs, a.batch, a.wstate, a.work, a.p, a.fallback);
   hipError_t e = hipGetLastError();
@@ -1422,8 +1422,7 @@ static hipError_t launch_wave(const LaunchArgs& a) {
   if constexpr (N <= 10) {
     if (schur_ok(a.p)) {
       hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs,
-                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback,
-                         a.spill);
+                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
       e = hipGetLastError();
       if (e != hipSuccess) return e;
       // the robots with (nearly) singular G_k, if any (an empty list costs one short launch)
@@ -1434,7 +1433,7 @@ static hipError_t launch_wave(const LaunchArgs& a) {
     }
   }
   hipLaunchKernelGGL((wv::wave_kernel<N, 0>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs, a.batch,
-                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback, nullptr);
+                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
   return hipGetLastError();
 }
 template <int N>
