@@ -40,7 +40,8 @@ def main():
         torch.cuda.synchronize()
         marks = tr.cpu().numpy().reshape(a.traced, 64, 4)
         res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
-    ph = {k: [] for k in ("setup", "factor", "f_pre", "f_buildS", "f_gj", "f_post", "iter_cycles", "check75", "ck_px", "ck_norms", "ck_tests", "ck_tail", "it_kkt",
+    ph = {k: [] for k in ("setup", "factor", "f_pre", "fp_rprime", "fp_rinv", "fp_b6r_g", "fp_chol", "fp_bvw",
+                          "fp_write", "f_buildS", "f_gj", "f_post", "iter_cycles", "check75", "ck_px", "ck_norms", "ck_tests", "ck_tail", "it_kkt",
                           "it_update", "it_rest", "total", "shader_ghz")}
     for b in range(a.traced):
         mk = marks[b]
@@ -58,6 +59,15 @@ def main():
             ph["f_buildS"].append(at[14][0] - at[13][0])
             ph["f_gj"].append(at[15][0] - at[14][0])
             ph["f_post"].append(at[12][0] - at[15][0])
+        if all(k in at for k in (21, 22, 23, 24, 25)):  # finer marks of the Schur prologue
+            ph["fp_rprime"].append(at[25][0] - at[10][0])
+            ph["fp_rinv"].append(at[21][0] - at[25][0])
+            ph["fp_b6r_g"].append(at[22][0] - at[21][0])
+            ph["fp_chol"].append(at[23][0] - at[22][0])
+            ph["fp_bvw"].append(at[24][0] - at[23][0])
+            ph["fp_write"].append(at[13][0] - at[24][0])
+        if 20 not in at:  # (trace full: a robot with many factorizations; skipped)
+            continue
         ph["total"].append(at[20][0] - at[0][0])
         ph["iter_cycles"].append((at[20][0] - at[4][0] - sum(fac)) / max(int(res["iters"][b]), 1))
         if 40 in at and 45 in at:
