@@ -3,23 +3,27 @@
 
 One step = one pass of the hot path over one batch of synthetic robot states resident in HBM:
 scale_kernel (OSQP scale_data on the condensed Hessian's closed-form columns) + wave_kernel
-(Riccati KKT factorization on MFMA, OSQP-0.6 ADMM, extraction), and for N > 1 ranks the RCCL
-all-gather of the solved forces over xGMI (north_star, config C3).
+(OSQP-0.6 ADMM with the KKT solve in the impulse-space Schur form at N <= 10, the Riccati form with
+its factorization on MFMA above; extraction) + the Riccati fallback launch for robots with
+rank-deficient feet (an empty list at C2), and for N > 1 ranks the RCCL all-gather of the solved
+forces over xGMI (north_star, config C3).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--horizon 10]
 
 --gpus N > 1 without a torch.distributed environment: this process starts
 `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child (it never touches the
 GPU itself) and exits with the child's code.  Every rank takes the contiguous shard
-shard_range(N*B, N, rank) of ONE seeded global batch of N*B robots (weak scaling: B robots per GPU;
-C3 = --gpus 8 --batch 8192), solves it and all-gathers u0 with mpcqp.distributed.allgather_forces.
+shard_range(N*B, N, rank) of ONE seeded global batch of N*B robots (weak scaling: B robots per GPU,
+8192 by default when N > 1, so --gpus 8 is C3's 65536 robots), solves it and all-gathers u0 with mpcqp.distributed.allgather_forces.
 Rank 0 checks the world size, checks the gathered forces against the CPU oracle on a 4096-robot
 sample spread over every shard, and prints ONE JSON line.
 
 At N = 1 the line also carries the CPU baseline (the oracle on the host cores) and extra keys,
 each with its own parity sample: e2e (host buffers in and out through mpcqp_solve_batch_host),
 assemble_e2e (raw robot-state rows -> on-device assembly -> solve), c4 (horizon 20), c5 (mixed
-gait, random mu, 8192 robots), warm_tick (closed-loop warm-started ticks).
+gait, random mu, 8192 robots), c3_shard (one GPU's 8192-robot share of C3), batch_scaling (4096 to
+65536 robots on one GPU), warm_tick (closed-loop warm-started ticks).  At N > 1 the line carries
+extras.allgather_ms (max over ranks of the per-step all-gather span).
 """
 import argparse
 import json
@@ -492,7 +496,11 @@ def extras(args, solver, params, recs_np, states, base_res, pyoracle, dev):
     fl = algorithmic_flops(20, g4["iters"], g4["rho_updates"])
     ent = {"value": B4 / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms, "batch": B4, "horizon": 20,
            "workload": "C4: horizon 20 (n=240, m=400), trot", "mean_iters": float(g4["iters"].mean()),
-           "roofline_frac": fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS}
+           "roofline_frac": fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+           # HBM bytes per launch of the N = 20 solve from its own rocprofv3 PMC pass (profiles/)
+           "traffic": load_traffic("N20_B4096_trot",
+                                   "mpcqp::wv::scale_kernel<20> + mpcqp::wv::wave_kernel<20, 0>"),
+           "kernels": "scale_kernel<20> + wave_kernel<20, 0> (Riccati form, factorization on MFMA)"}
     if pyoracle is not None:
         idx = np.unique(np.linspace(0, B4 - 1, 256).astype(np.int64))
         ref = pyoracle.solve_batch(pyoracle.default_params(20), rec4[idx], nthreads=nthr)
