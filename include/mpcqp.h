@@ -35,7 +35,7 @@ extern "C" {
 #define MPCQP_NUM_LEG 4         /* NUM_LEG (FL, FR, RL, RR)                               */
 #define MPCQP_NUM_DOF 12        /* NUM_DOF: 3 GRF components x 4 legs per horizon step     */
 #define MPCQP_CONSTRAINT_DIM 20 /* MPC_CONSTRAINT_DIM: 5 friction-pyramid rows x 4 legs    */
-#define MPCQP_MAX_HORIZON 20    /* 1..20: one-wavefront-per-robot Riccati path (default)       */
+#define MPCQP_MAX_HORIZON 20    /* 1..20: one wavefront per robot (Schur form N<=10, Riccati N>10) */
 #define MPCQP_OSQP_INFTY 1e30   /* OsqpEigen::INFTY == OSQP_INFTY (OSQP 0.6 constants.h)  */
 
 /* ---- per-instance problem record (all binary64, contiguous) ----------------------------

@@ -28,8 +28,9 @@ int32_t mpcqp_handle_slots(mpcqp_handle* h);
 /* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */
 int32_t mpcqp_solve_threads(int32_t horizon);
 
-/* Select the linear-system path of a handle: 0 auto (= 3), 3 Riccati with one wavefront per
- * robot (the product path).  The debug build libmpcqp_debug.so adds two cross-check solvers:
+/* Select the linear-system path of a handle: 0 auto (= 3), 3 the product path, one wavefront per
+ * robot (impulse-space Schur form for N <= 10 with the Riccati form for robots whose feet are
+ * degenerate; Riccati form for N > 10).  The debug build libmpcqp_debug.so adds two cross-check solvers:
  * 1 dense K^-1 with one workgroup per robot (N <= 10), 2 Riccati with one workgroup per robot.
  * All paths run the same OSQP iteration; the selection exists to cross-check them on the same
  * inputs.  The product libmpcqp.so returns MPCQP_ERR_INVALID_ARG for 1 and 2. */

@@ -169,6 +169,10 @@ class Lazy {
   auto size() const -> decltype(std::declval<const U&>().size()) { return get().size(); }
   const double* data() const { return get().data(); }
   template <class U = T>
+  auto rows() const -> decltype(std::declval<const U&>().rows()) { return get().rows(); }
+  template <class U = T>
+  auto cols() const -> decltype(std::declval<const U&>().cols()) { return get().cols(); }
+  template <class U = T>
   auto begin() const -> decltype(std::declval<const U&>().begin()) { return get().begin(); }
   template <class U = T>
   auto end() const -> decltype(std::declval<const U&>().end()) { return get().end(); }

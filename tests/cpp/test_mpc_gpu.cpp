@@ -86,11 +86,31 @@ int main() {
     mpc_solver.B_mat_d_list.block<13, 12>(i * 13, 0) = mpc_solver.B_mat_d;  // :121, verbatim
   }
   mpc_solver.calculate_qp_mats(state);  // :125
+  // the large members are produced on first read (nothing has been read yet)
+  std::printf("LAZY_BEFORE %d %d %d %d %d\n", (int)mpc_solver.hessian.computed(), (int)mpc_solver.gradient.computed(),
+              (int)mpc_solver.linear_constraints.computed(), (int)mpc_solver.A_qp.computed(),
+              (int)mpc_solver.B_qp.computed());
   double hsum = 0, hmax = 0, gsum = 0;
   for (double v : mpc_solver.hessian) { hsum += v; hmax = v > hmax ? v : hmax; }
   for (double v : mpc_solver.gradient) gsum += v;
   std::printf("HESSIAN_SUM %.17g\nHESSIAN_MAX %.17g\nGRADIENT_SUM %.17g\n", hsum, hmax, gsum);
   std::printf("HESSIAN_00 %.17g\n", mpc_solver.hessian[0]);
+  std::printf("LAZY_AFTER_H %d %d %d %d %d\n", (int)mpc_solver.hessian.computed(), (int)mpc_solver.gradient.computed(),
+              (int)mpc_solver.linear_constraints.computed(), (int)mpc_solver.A_qp.computed(),
+              (int)mpc_solver.B_qp.computed());
+  // A_qp (13N x 13) and B_qp (13N x 12N) of ConvexMpc.cpp:184-202, read like the Eigen members
+  std::printf("A_QP %d %d", (int)mpc_solver.A_qp.rows(), (int)mpc_solver.A_qp.cols());
+  for (int i = 0; i < mpc_solver.A_qp.rows(); ++i)
+    for (int j = 0; j < mpc_solver.A_qp.cols(); ++j) std::printf(" %.17g", mpc_solver.A_qp(i, j));
+  std::printf("\nB_QP %d %d", (int)mpc_solver.B_qp.rows(), (int)mpc_solver.B_qp.cols());
+  for (int i = 0; i < mpc_solver.B_qp.rows(); ++i)
+    for (int j = 0; j < mpc_solver.B_qp.cols(); ++j) std::printf(" %.17g", mpc_solver.B_qp(i, j));
+  std::printf("\nA_MAT_D");
+  for (int i = 0; i < 13; ++i)
+    for (int j = 0; j < 13; ++j) std::printf(" %.17g", mpc_solver.A_mat_d(i, j));
+  std::printf("\nLIN_CON %d", (int)mpc_solver.linear_constraints.size());
+  for (double v : mpc_solver.linear_constraints) std::printf(" %.17g", v);
+  std::printf("\n");
 
   // :131-151 solve (fresh solver, cold start) through the C ABI
   mpcqp_result res;

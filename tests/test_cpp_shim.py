@@ -21,8 +21,12 @@ def test_cpp_test_mpc_harness(oracle):
     rows, grf, grf_sim = [], [], []
     for line in out.splitlines():
         parts = line.split()
-        if parts[0] in ("RECOVERED_FEET", "RECORD"):
+        if parts[0] in ("RECOVERED_FEET", "RECORD", "A_MAT_D", "LIN_CON"):
             kv[parts[0]] = np.array([float(x) for x in parts[1:]])
+        elif parts[0] in ("A_QP", "B_QP"):
+            kv[parts[0]] = np.array([float(x) for x in parts[3:]]).reshape(int(parts[1]), int(parts[2]))
+        elif parts[0].startswith("LAZY_"):
+            kv[parts[0]] = [int(x) for x in parts[1:]]
         elif parts[0] == "STAGING_DEVICE":
             kv["staging_device"], kv["handle_device"] = int(parts[1]), int(parts[3])
         elif parts[0] == "ROW":
@@ -45,6 +49,31 @@ def test_cpp_test_mpc_harness(oracle):
     u0 = np.array(rows).T.reshape(12)  # [leg][xyz]
     assert np.max(np.abs(u0 - ref["u0"])) <= 1e-4 * max(np.max(np.abs(ref["u0"])), 1)
     assert (kv["status"], kv["iters"], kv["rho_updates"]) == (int(ref["status"]), int(ref["iters"]), int(ref["rho_updates"]))
+    # lazy members: nothing produced by calculate_qp_mats itself; one device round trip fills
+    # hessian and gradient together, the host-side members stay unproduced until read
+    assert kv["LAZY_BEFORE"] == [0, 0, 0, 0, 0]
+    assert kv["LAZY_AFTER_H"] == [1, 1, 0, 0, 0]
+    # A_qp / B_qp (ConvexMpc.cpp:184-202): A_qp block i = A_d^(i+1), B_qp lower block-triangular,
+    # and the reference's H = B_qp' Q B_qp + R, g = B_qp' Q (A_qp x0 - x_ref) (:207-217) with
+    # Q = diag(2 q), R = diag(2 r) (ConvexMpc.cpp:20, :42) reproduce the oracle's P and q
+    Ad = kv["A_MAT_D"].reshape(13, 13)
+    Aqp, Bqp = kv["A_QP"], kv["B_QP"]
+    assert Aqp.shape == (130, 13) and Bqp.shape == (130, 120)
+    M = np.eye(13)
+    for i in range(10):
+        M = M @ Ad
+        np.testing.assert_allclose(Aqp[13 * i:13 * i + 13], M, rtol=0, atol=1e-12 * max(1, np.abs(M).max()))
+        assert np.all(Bqp[13 * i:13 * i + 13, 12 * (i + 1):] == 0)
+    Qd = np.tile(2 * np.asarray(q, dtype=np.float64), 10)
+    Rd = np.tile(2 * np.asarray(r, dtype=np.float64), 10)
+    H2 = Bqp.T @ (Qd[:, None] * Bqp) + np.diag(Rd)
+    np.testing.assert_allclose(H2, P, rtol=0, atol=1e-10 * np.abs(P).max())
+    x0 = rec[mpcqp._lib.REC_X0:mpcqp._lib.REC_X0 + 13]
+    xr = rec[mpcqp._lib.REC_XREF:mpcqp._lib.REC_XREF + 130]
+    g2 = Bqp.T @ (Qd * (Aqp @ x0 - xr))
+    np.testing.assert_allclose(g2, g, rtol=0, atol=1e-10 * max(np.abs(g).max(), 1e-12))
+    assert int(kv["LIN_CON"][0]) == A.size
+    np.testing.assert_array_equal(kv["LIN_CON"][1:].reshape(A.shape), A)
     # the formulation's device staging is on the handle's device
     assert kv["staging_device"] == kv["handle_device"]
     # B_mat_d_list block 3 replaced by a B_d of feet moved +0.01 in x: read back through I_w
