@@ -360,6 +360,15 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     __syncthreads();
   }
   SC_MARK(3);
+  // Column norms without H.  cm0 = max_i |H_ij| (the raw pass, D = 1) and Dmax = max_i D_i bound
+  // every later norm: fl(D_i |H_ij|) <= fl(Dmax cm0_j) (rounding is monotone), so ub_j = Dmax cm0_j
+  // >= cm_j, and sums of the same shape keep the order.  Where the bounds already decide both uses
+  // of cm — the cost normalization (mean of c D_j cm_j at most inf_norm_q, so c_temp comes from q
+  // alone) and the next pass's fmax(c D_j cm_j, |A~ col j|) (the A~ side wins) — the exact norms
+  // cannot change a bit of the result and are not computed; otherwise the pass regenerates them.
+  // (Go1 workloads: every pass of every robot is decided by the bounds, H's entries being far
+  // below A's unit entries.)
+  const double cm0 = cm;
   for (int pass = 0; pass < p.scaling; ++pass) {
     if (pass == 1) SC_MARK(4);
     // new scaling factors from the current D, E (every thread reads before anyone writes)
@@ -381,25 +390,54 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
       const int r = t + NTS * rr;
       if (r < m) En[r] = Ec[r] * et[rr];
     }
+    double dmx = 0.0;
     if (lead && j0 < n) {
       sm.q[j0] = dtv * sm.q[j0];
       Dn[j0] = Dc[j0] * dtv;
+      dmx = Dn[j0];
     }
+    dmx = wave_max(dmx);
+    if ((t & 63) == 0) sm.dmx[t >> 6] = dmx;
     __syncthreads();
     Dc = Dn;
     Ec = En;
-    cm = colmax(false);  // column norms of the D-scaled P (cost normalization)
-    double sv = 0.0, qv = 0.0;
-    if (lead && j0 < n) {
-      sv = (c_s * Dc[j0]) * cm;
-      qv = dabs(sm.q[j0]);
+    double dmax_all = sm.dmx[0];
+#pragma unroll
+    for (int w = 1; w < SC::NWS; ++w) dmax_all = fmax(dmax_all, sm.dmx[w]);
+    const double ub = dmax_all * cm0;  // >= this pass's column norm of the D-scaled P
+    double c_temp;
+    bool exact;
+    {
+      double sv = 0.0, qv = 0.0;
+      if (lead && j0 < n) {
+        sv = (c_s * Dc[j0]) * ub;
+        qv = dabs(sm.q[j0]);
+      }
+      block_sum_max<SC::NWS>(sv, qv, sm.redb);
+      const double inf_norm_q = limit_scaling(qv);
+      exact = !(sv / n <= inf_norm_q);  // (block-uniform)
+      c_temp = 1. / limit_scaling(inf_norm_q);
+      if (pass + 1 < p.scaling) {  // the next pass's dtv: c_new D_j ub_j <= |A~ col j| everywhere?
+        const bool bad = !exact && lead && j0 < n && !(((c_s * c_temp) * Dc[j0]) * ub <= acol(j0));
+        exact = __syncthreads_or(exact || bad) != 0;
+      }
     }
-    block_sum_max<SC::NWS>(sv, qv, sm.red);
-    double c_temp = sv / n;
-    const double inf_norm_q = limit_scaling(qv);
-    c_temp = dmax(c_temp, inf_norm_q);
-    c_temp = limit_scaling(c_temp);
-    c_temp = 1. / c_temp;
+    if (exact) {
+      cm = colmax(false);  // column norms of the D-scaled P (cost normalization)
+      double sv = 0.0, qv = 0.0;
+      if (lead && j0 < n) {
+        sv = (c_s * Dc[j0]) * cm;
+        qv = dabs(sm.q[j0]);
+      }
+      block_sum_max<SC::NWS>(sv, qv, sm.red);
+      c_temp = sv / n;
+      const double inf_norm_q = limit_scaling(qv);
+      c_temp = dmax(c_temp, inf_norm_q);
+      c_temp = limit_scaling(c_temp);
+      c_temp = 1. / c_temp;
+    } else {
+      cm = ub;  // the next pass's fmax picks the A~ norm either way
+    }
     if (lead && j0 < n) sm.q[j0] *= c_temp;  // own column only: no barrier before the next pass
     c_s *= c_temp;
   }

@@ -575,6 +575,8 @@ struct ScaleSmem {
   double vec[2][16];
   double Ap[2][C::m];
   double red[2][16];
+  double redb[2][16];  // the bound test's sums (a buffer of its own: no barrier against red's reads)
+  double dmx[16];      // per-wave max of the new D
 };
 
 // block-wide sum of sv and max of qv in one barrier (wave partials summed in wave order)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """scale_kernel phase timing: run a library built with -DMPCQP_SCALE_TIMING (tools/build_variant.sh
-OUT.so 10 -DMPCQP_SCALE_TIMING, selected with MPCQP_LIB); thread 0 of each robot writes {id,
+OUT.so 10 -DMPCQP_SCALE_TIMING, selected with MPCQP_LIB; MPCQP_N=20 for another horizon); thread 0 of each robot writes {id,
 s_memtime} pairs over its own record.  Reports median shader-clock cycles per phase: 0 -> 1 record
 load + B_w + gradient sweeps, 1 -> 2 column init, 2 -> 3 first column pass (H columns generated),
 3 -> 4 Ruiz pass 0, 4 -> 5 passes 1..9, 5 -> 6 image write; and the robot's whole span."""
@@ -16,9 +16,10 @@ sys.path.insert(0, os.path.join(REPO, "go1-qp-mpc-controller_amd"))
 import mpcqp  # noqa: E402
 
 B = 4096
+NH = int(os.environ.get("MPCQP_N", "10"))  # horizon (the variant library must be built for it)
 st = mpcqp.synthetic_go1(B, seed=1000, gait="trot")
-recs = mpcqp.assemble_compute_grf(st, 10)
-with mpcqp.MpcQpSolver(mpcqp.default_params(10, max_iter=1)) as s:
+recs = mpcqp.assemble_compute_grf(st, NH)
+with mpcqp.MpcQpSolver(mpcqp.default_params(NH, max_iter=1)) as s:
     d_res = torch.zeros((B, mpcqp._lib.RESULT_DOUBLES), dtype=torch.float64, device="cuda")
     for _ in range(3):
         d_rec = torch.from_numpy(recs).cuda()
