@@ -793,6 +793,21 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
   // KS = 0: 2 q_j of the MFMA column j = lane & 15 (factorize_mfma's cQ diagonal)
   double Q2J = KS == 0 ? 2.0 * p.q_weights[li < ND ? li : 0] : 0.0;
   keep(Q2J);
+  // KS = 0 without stored Acl: the lane's coefficients of A' on states 0-5 (lane of state i: A[s][i])
+  // and of A on states 6-11 (A[i][6 + s]), the off-diagonal part of the discrete A
+  constexpr bool NOACL = KS == 0 && !WSmem<N, KS>::SACL;
+  double CAT[NOACL ? 6 : 1], CAX[NOACL ? 6 : 1];
+  if constexpr (NOACL) {
+    const int si = 3 * leg + (a < 3 ? a : 0);  // the lane's state (a = 3: padding)
+    const bool sv = a < 3;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      CAT[e] = sv && si >= 6 ? A.at(e, si) : 0.0;
+      CAX[e] = sv && si < 6 ? A.at(si, 6 + e) : 0.0;
+    }
+  }
+  (void)CAT;
+  (void)CAX;
   // KS = 1: the lane's rows of R'^-1 (mpcqp_schur.h), set per rho
   double SRI[KS == 1 ? R : 1][3];
   (void)SRI;
@@ -853,7 +868,7 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
           const double ib = b == 0 ? i0 : (b == 1 ? i1 : i2);
           const double rt = (av && a == b ? cost_c * R2I : 0.0) + (ia * ((av && a == b ? sigma : 0.0) + s)) * ib;
           if (kvr[r] && av && b >= a) {
-            if constexpr (KS == 0) F.Rt[k][leg][sym6(a, b)] = rt;
+            if constexpr (KS == 0) F.rt(k)[6 * leg + sym6(a, b)] = rt;
             else F.s.Rt[k][leg][sym6(a, b)] = rt;
           }
         }
@@ -889,6 +904,104 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
         schur_solve<N, R>(F, W2, SRI, vvr, U);
       }
 #endif
+    } else if constexpr (NOACL) {
+      // Riccati form without Acl (sigma_k = -s_k):
+      //   backward  t_k = w_k - B_k' sigma_{k+1},  sigma_k = K_k' t_k + A' sigma_{k+1}  (sigma_N = 0)
+      //   parallel  g_k = G_k^-1 t_k
+      //   forward   u_k = g_k - K_k x_k,  x_{k+1} = A x_k + B_k u_k                    (x_0 = 0)
+      // (the same recursion: s_k = Acl_k' s_{k+1} - K_k' w_k, x_{k+1} = Acl_k x_k + B_k g_k)
+      double W[R], TT[R], G[R];
+      int kc[R], kk[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        W[r] = DI[r] * RHS[r];
+        TT[r] = 0.0;
+        U[r] = 0.0;
+        kc[r] = min(4 * r + ig, N - 1);
+        kk[r] = max(kc[r] - 1, 0);  // slot of K_k (k >= 1)
+      }
+      if (tm_it) WV_MARK(41);
+      {  // backward chain; a round's K_k columns (rows of K_k') serve its four steps, one per row
+        double kn[12], kcur[12], bcur[6];
+        ldcol(kn, &F.K[kk[(N - 1) >> 2]][idx]);
+        double cur = 0.0;
+        sfor<0, N>([&](auto J) {
+          constexpr int k = N - 1 - decltype(J)::value;
+          constexpr int r = k >> 2;
+          if constexpr (k == N - 1 || (k & 3) == 3) {  // entering round r (descending)
+            lds_wait<0>(kn);
+#pragma unroll
+            for (int e = 0; e < 12; ++e) kcur[e] = kn[e];
+            if constexpr (r >= 1) ldcol(kn, &F.K[kk[r - 1]][idx]);
+            bcur[0] = -sm.Bw[kc[r]][0][idx];
+            bcur[1] = -sm.Bw[kc[r]][1][idx];
+            bcur[2] = -sm.Bw[kc[r]][2][idx];
+            bcur[3] = a == 0 ? -dtm : 0.0;
+            bcur[4] = a == 1 ? -dtm : 0.0;
+            bcur[5] = a == 2 ? -dtm : 0.0;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          double m = 0.0, tk = W[r];
+          if constexpr (k < N - 1) {
+            m = rmove2<row_of(k + 1), row_of(k)>(cur);
+            tk = mv6a(m, bcur, W[r]);
+          }
+          TT[r] = (q == row_of(k)) ? tk : TT[r];
+          if constexpr (k >= 1) {
+            const double as = k < N - 1 ? mv6lo_a(m, CAT, m) : 0.0;
+            cur = mv12a(tk, kcur, as);
+          }
+        });
+      }
+      if (tm_it) WV_MARK(42);
+      // g_k = G_k^-1 t_k
+      {
+        double c0[12], c1[12];
+        ld12(c0, &F.Gi[kc[0]][mo(idx)]);
+        sfor<0, R>([&](auto RR) {
+          constexpr int r = decltype(RR)::value;
+          if constexpr (r + 1 < R) ld12((r & 1) ? c0 : c1, &F.Gi[kc[r + 1]][mo(idx)]);
+          G[r] = mv12(TT[r], (r & 1) ? c1 : c0);
+        });
+      }
+      if (tm_it) WV_MARK(43);
+      {  // forward chain; a round's K_k rows and B_w rows serve its four steps
+        double kn[12], kcur[12], bn[12], bcu[12];
+        ld12(kn, &F.K[kk[0]][mo(idx)]);
+        ld12(bn, &sm.Bw[kc[0]][av ? a : 2][0]);
+        double cur = 0.0;
+        sfor<0, N>([&](auto K) {
+          constexpr int k = decltype(K)::value;
+          constexpr int r = k >> 2;
+          if constexpr ((k & 3) == 0) {  // entering round r (ascending)
+#pragma unroll
+            for (int e = 0; e < 12; ++e) {
+              kcur[e] = kn[e];
+              bcu[e] = bn[e];
+            }
+            if constexpr (r + 1 < R) {
+              ld12(kn, &F.K[kk[r + 1]][mo(idx)]);
+              ld12(bn, &sm.Bw[kc[r + 1]][av ? a : 2][0]);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          double m = 0.0, nu = -G[r];  // nu = -u_k = K_k x_k - g_k
+          if constexpr (k >= 1) {
+            m = rmove2<row_of(k - 1), row_of(k)>(cur);
+            nu = mv12a(m, kcur, -G[r]);
+          }
+          U[r] = (q == row_of(k)) ? -nu : U[r];
+          if constexpr (k <= N - 2) {
+            // B_k nu: rows 6-8 (leg-2 lanes) B_w nu, rows 9-11 (leg-3 lanes) dt/m times the legs' sum
+            const double hb = mv12(nu, bcu);
+            const double ls = dtm * legsum(nu);
+            const double bnu = leg == 2 ? hb : (leg == 3 ? ls : 0.0);
+            const double ax = k >= 1 ? mv6a(m, CAX, m) : 0.0;  // A x_k
+            cur = ax - bnu;
+          }
+        });
+      }
+      if (tm_it) WV_MARK(44);
     } else {
       // LDS operands are loaded one phase ahead of their use; sched_barrier keeps the scheduler from
       // sinking a prefetch back down to its consumer (counted lgkmcnt waits then cover only it).

@@ -45,11 +45,40 @@ __host__ __device__ constexpr int mo(int r) { return 12 * r + (r >= 4 ? 2 : 0); 
 
 template <int N>
 struct SchurLds;
+// Riccati factors (KS = 0; the factorization itself runs in registers).  With SACL the closed-loop
+// matrices Acl_k = A - B_k K_k are stored for the chains; without (long horizons: the three factor
+// families would leave room for only two robots per CU) the chains apply A and B_k K_k separately,
+// and the R'_k foot blocks share G_k^-1's slot (read by factorization step k before it writes G_k^-1).
+#ifndef MPCQP_ACL_MAXN
+#define MPCQP_ACL_MAXN 20
+#endif
+template <int N, bool SACL>
+struct RicFactors;
+template <int N>
+struct RicFactors<N, true> {
+  static constexpr bool HAS_ACL = true;
+  static constexpr int NK = N > 1 ? N - 1 : 1;  // K_k stored for k = 1..N-1
+  static constexpr int NA = N > 2 ? N - 2 : 1;  // Acl_k stored for k = 1..N-2
+  alignas(16) double Gi[N][MS];
+  alignas(16) double K[NK][MS];
+  alignas(16) double Acl[NA][MS];
+  double Rt[N][4][6];  // R'_k foot blocks, upper triangle (00 01 02 11 12 22)
+  __device__ double* rt(int k) { return &Rt[k][0][0]; }
+};
+template <int N>
+struct RicFactors<N, false> {
+  static constexpr bool HAS_ACL = false;
+  static constexpr int NK = N > 1 ? N - 1 : 1;
+  alignas(16) double Gi[N][MS];
+  alignas(16) double K[NK][MS];
+  __device__ double* rt(int k) { return &Gi[k][0]; }
+};
 template <int N, int KS>
 struct WSmem {
   using C = Cfg<N>;
+  static constexpr bool SACL = N <= MPCQP_ACL_MAXN;
   static constexpr int NK = N > 1 ? N - 1 : 1;  // K_k stored for k = 1..N-1
-  static constexpr int NA = N > 2 ? N - 2 : 1;  // Acl_k stored for k = 1..N-2
+  static constexpr int NA = N > 2 ? N - 2 : 1;  // Acl_k stored for k = 1..N-2 (SACL)
   alignas(16) double Bw[N][3][ND];  // rows 6-8 of B_d(k) = I_w^-1 skew(foot) dt (rows 9-11: dt/m I)
   union U {
     struct Hs {  // setup: record, Ruiz vectors
@@ -59,14 +88,8 @@ struct WSmem {
       double vec[2][16];  // sequential 13-vectors (gradient forward sweep)
       double qn[C::n];     // this tick's gradient (warm start: q of the Ruiz passes is the old one)
     } h;
-    struct Fs {  // solve: per-step factors (the factorization itself runs in registers)
-      alignas(16) double Gi[N][MS];
-      alignas(16) double K[NK][MS];
-      alignas(16) double Acl[NA][MS];
-      double Rt[N][4][6];             // R'_k foot blocks, upper triangle (00 01 02 11 12 22)
-    };
     // KS = 0: the Riccati factors; KS = 1: the impulse-space Schur form (mpcqp_schur.h)
-    typename std::conditional<KS == 0, Fs, SchurLds<N>>::type f;
+    typename std::conditional<KS == 0, RicFactors<N, SACL>, SchurLds<N>>::type f;
   } u;
 };
 
@@ -162,6 +185,29 @@ __device__ __forceinline__ double mv12a(double x, const double (&c)[12], double 
       : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
         [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]),
         [c11] "v"(c[11]));
+  return (a1 + a2) + a0;
+}
+
+// init + sum over states 6..11 (lanes 8, 9, 10, 12, 13, 14) of c[s-6] x_s
+__device__ __forceinline__ double mv6a(double x, const double (&c)[6], double init) {
+  double a0 = init, a1 = 0.0, a2 = 0.0;
+  asm("s_nop 4\n\t"
+      WV_FM("%[a1]", "%[c0]", 8) WV_FM("%[a2]", "%[c1]", 9) WV_FM("%[a0]", "%[c2]", 10)
+      WV_FM("%[a1]", "%[c3]", 12) WV_FM("%[a2]", "%[c4]", 13) WV_FM("%[a0]", "%[c5]", 14)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
+        [c5] "v"(c[5]));
+  return (a1 + a2) + a0;
+}
+// init + sum over states 0..5 (lanes 0, 1, 2, 4, 5, 6) of c[s] x_s
+__device__ __forceinline__ double mv6lo_a(double x, const double (&c)[6], double init) {
+  double a0 = init, a1 = 0.0, a2 = 0.0;
+  asm("s_nop 4\n\t"
+      WV_FM("%[a1]", "%[c0]", 0) WV_FM("%[a2]", "%[c1]", 1) WV_FM("%[a0]", "%[c2]", 2)
+      WV_FM("%[a1]", "%[c3]", 4) WV_FM("%[a2]", "%[c4]", 5) WV_FM("%[a0]", "%[c5]", 6)
+      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
+        [c5] "v"(c[5]));
   return (a1 + a2) + a0;
 }
 
@@ -485,7 +531,7 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
       Bt[v] = bsc(j, u);
       // R'_k: 3x3 foot blocks (upper triangle stored); identity on the pad
       double rv = 0.0;
-      if (u < 12 && j < 12 && u / 3 == j / 3) rv = F.Rt[k][u / 3][sym6(u % 3, j % 3)];
+      if (u < 12 && j < 12 && u / 3 == j / 3) rv = F.rt(k)[6 * (u / 3) + sym6(u % 3, j % 3)];
       if (u >= 12 && u == j) rv = 1.0;
       G[v] = rv;
     }
@@ -507,14 +553,16 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
       if (j < 12)
 #pragma unroll
         for (int v = 0; v < 3; ++v) F.K[k - 1][mo(4 * v + grp) + j] = K[v];
-      if (k <= N - 2) {
-        mf4 nBt;
+      if constexpr (std::remove_reference_t<decltype(F)>::HAS_ACL) {
+        if (k <= N - 2) {
+          mf4 nBt;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) nBt[v] = -Bt[v];
-        const mf4 Acl = mfma_chain<0, 3>(nBt, K, Ad);       // A - B K
-        if (j < 12)
+          for (int v = 0; v < 4; ++v) nBt[v] = -Bt[v];
+          const mf4 Acl = mfma_chain<0, 3>(nBt, K, Ad);       // A - B K
+          if (j < 12)
 #pragma unroll
-          for (int v = 0; v < 3; ++v) F.Acl[k - 1][mo(4 * v + grp) + j] = Acl[v];
+            for (int v = 0; v < 3; ++v) F.Acl[k - 1][mo(4 * v + grp) + j] = Acl[v];
+        }
       }
       mf4 nF;
 #pragma unroll

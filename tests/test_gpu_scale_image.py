@@ -121,3 +121,24 @@ def test_scale_image_warm_branches_match_oracle(oracle):
     for w in ws:
         w.close()
     assert modes == {0, 1, 2}, modes
+
+
+def test_scale_image_matches_oracle_on_c4_sample(oracle):
+    """Horizon 20 (C4): the Riccati-form solve reads the same image."""
+    st = mpcqp.synthetic_go1(4096, seed=1000, gait="trot")
+    recs = mpcqp.assemble_compute_grf(st, 20)
+    idx = np.unique(np.linspace(0, 4095, 64).astype(np.int64))
+    _check_cold(oracle, recs[idx], 20, label="C4")
+
+
+@pytest.mark.parametrize("N,qs,rs", [(10, 1e4, 1e4), (10, 1e6, 1.0), (20, 1e5, 1e3)])
+def test_scale_image_heavy_weights_exercise_exact_passes(oracle, N, qs, rs):
+    """Weights large enough that D H D's column norms matter: the passes the bound cannot decide
+    (scale_kernel regenerates H's columns there) and those it can, in one batch; both must give the
+    oracle's scale_data.  (With the Go1 weights every pass is decided by the bound.)"""
+    st = mpcqp.synthetic_go1(64, seed=7, gait="trot")
+    recs = mpcqp.assemble_compute_grf(st, N)
+    p0 = mpcqp.default_params(N)
+    q = [w * qs for w in p0.q_weights]
+    r = [w * rs for w in p0.r_weights]
+    _check_cold(oracle, recs, N, q=q, r=r, label=f"N{N} q*{qs:g} r*{rs:g}")

@@ -42,7 +42,7 @@ def main():
         res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
     ph = {k: [] for k in ("setup", "factor", "f_pre", "fp_rprime", "fp_rinv", "fp_b6r_g", "fp_chol", "fp_bvw",
                           "fp_write", "f_buildS", "f_gj", "f_post", "iter_cycles", "check75", "ck_px", "ck_norms", "ck_tests", "ck_tail", "it_kkt",
-                          "it_update", "it_rest", "total", "shader_ghz")}
+                          "it_update", "it_rest", "kkt_a", "kkt_back", "kkt_g", "kkt_fwd", "kkt_u", "total", "shader_ghz")}
     for b in range(a.traced):
         mk = marks[b]
         mk = mk[~np.isnan(mk[:, 0])]
@@ -74,6 +74,12 @@ def main():
             ph["it_kkt"].append(at[45][0] - at[40][0])
             ph["it_update"].append(at[46][0] - at[45][0])
             ph["it_rest"].append(at[47][0] - at[46][0])
+            if all(k in at for k in (41, 42, 43, 44)):  # Riccati-form KKT sub-phases
+                ph["kkt_a"].append(at[41][0] - at[40][0])
+                ph["kkt_back"].append(at[42][0] - at[41][0])
+                ph["kkt_g"].append(at[43][0] - at[42][0])
+                ph["kkt_fwd"].append(at[44][0] - at[43][0])
+                ph["kkt_u"].append(at[45][0] - at[44][0])
         if 48 in at and 49 in at:
             ph["check75"].append(at[49][0] - at[48][0])
         if all(k in at for k in (48, 50, 51, 52, 49)):
