@@ -360,84 +360,176 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     __syncthreads();
   }
   SC_MARK(3);
-  // Column norms without H.  cm0 = max_i |H_ij| (the raw pass, D = 1) and Dmax = max_i D_i bound
-  // every later norm: fl(D_i |H_ij|) <= fl(Dmax cm0_j) (rounding is monotone), so ub_j = Dmax cm0_j
-  // >= cm_j, and sums of the same shape keep the order.  Where the bounds already decide both uses
-  // of cm — the cost normalization (mean of c D_j cm_j at most inf_norm_q, so c_temp comes from q
-  // alone) and the next pass's fmax(c D_j cm_j, |A~ col j|) (the A~ side wins) — the exact norms
-  // cannot change a bit of the result and are not computed; otherwise the pass regenerates them.
-  // (Go1 workloads: every pass of every robot is decided by the bounds, H's entries being far
-  // below A's unit entries.)
-  const double cm0 = cm;
-  for (int pass = 0; pass < p.scaling; ++pass) {
-    if (pass == 1) SC_MARK(4);
-    // new scaling factors from the current D, E (every thread reads before anyone writes)
-    double dtv = 1.0;
-    if (lead && j0 < n) {
-      const double pc = (c_s * Dc[j0]) * cm;
-      dtv = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j0))));
-    }
-    double et[SC::RPT];
+  // Ruiz passes decided by bounds.  A pass uses the column norms cm_j = max_i D_i |H_ij| of the
+  // D-scaled P twice: in the cost normalization (c_temp = 1 / max(mean_j c D_j cm_j, |q|_inf)) and
+  // in the next pass's fmax(c D_j cm_j, |A~ col j|).  With cm0_j = max_i |H_ij| (the raw pass,
+  // D = 1) and Dmax = max_i D_i, fl(D_i |H_ij|) <= fl(Dmax cm0_j) (rounding is monotone); where
+  // these bounds, with a margin for the roundings of the sums and products, already let |q|_inf win
+  // the normalization and the A~ norm win every column's fmax, the exact norms cannot change a bit
+  // of the result.  Such a pass is per-foot work — A is block diagonal over the feet (5 rows x 3
+  // columns) — done by one thread per foot in place, plus one block reduction (sum c D_j cm0_j,
+  // max |q_j|, max D_j, min_j |A~ col j| / (D_j cm0_j)).  The first pass the bounds cannot decide
+  // and all after it run the exact passes below.  (Go1 workloads: every pass of every robot is
+  // decided by the bounds, H's entries being far below A's unit entries.)
+  if (lead && j0 < n) sm.cm0[j0] = cm;
+  __syncthreads();
+  int pass = 0;
+  bool resume = false;  // the bound passes stopped after the D, E, q update of `pass`
+  {
+    constexpr int NF = 4 * N;
+    constexpr double EPS = 2.220446049250313e-16;
+    constexpr double M1 = 1.0 + 4.0 * (n + 8) * EPS;  // sum / product margin of the normalization test
+    constexpr double M2 = 1.0 + 16.0 * EPS;           // product margin of the fmax test
+    double dmax_prev = 1.0;                           // Dmax of the previous pass (ub_j = Dmax cm0_j)
+    for (; pass < p.scaling; ++pass) {
+      if (pass == 1) SC_MARK(4);
+      double s0 = 0.0, qm = 0.0, dm = 0.0, rmin = INFINITY;
+      if (t < NF) {
+        const int f = t;
+        double e[5], a0[5], a1[5], d[3], cz[3];
 #pragma unroll
-    for (int rr = 0; rr < SC::RPT; ++rr) {
-      const int r = t + NTS * rr;
-      et[rr] = r < m ? 1.0 / sqrt(limit_scaling(arow(r))) : 1.0;
-    }
-    double* const Dn = sm.D[(pass + 1) & 1];
-    double* const En = sm.E[(pass + 1) & 1];
+        for (int i = 0; i < 5; ++i) {
+          e[i] = Ec[5 * f + i];
+          a0[i] = sm.Ap[0][5 * f + i];
+          a1[i] = sm.Ap[1][5 * f + i];
+        }
 #pragma unroll
-    for (int rr = 0; rr < SC::RPT; ++rr) {
-      const int r = t + NTS * rr;
-      if (r < m) En[r] = Ec[r] * et[rr];
+        for (int i = 0; i < 3; ++i) {
+          d[i] = Dc[3 * f + i];
+          cz[i] = sm.cm0[3 * f + i];
+        }
+        // |A~ col| of the foot's fx, fy, fz columns without D (acol above, same operations)
+        auto acol3 = [&](const double (&ee)[5], double (&mc)[3]) __attribute__((always_inline)) {
+          mc[0] = dmax(ee[0] * dabs(a0[0]), ee[1] * dabs(a0[1]));
+          mc[1] = dmax(ee[2] * dabs(a0[2]), ee[3] * dabs(a0[3]));
+          mc[2] = dmax(dmax(dmax(dmax(dabs(a1[0]) * ee[0], dabs(a1[1]) * ee[1]), dabs(a1[2]) * ee[2]),
+                            dabs(a1[3]) * ee[3]),
+                       ee[4] * dabs(a1[4]));
+        };
+        double mc[3];
+        acol3(e, mc);
+        double dtv[3], et[5];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const double cmj = pass == 0 ? cz[i] : dmax_prev * cz[i];
+          const double pc = (c_s * d[i]) * cmj;
+          dtv[i] = 1.0 / sqrt(limit_scaling(fmax(pc, mc[i] * d[i])));
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {  // arow above
+          const double dk = d[i < 4 ? i >> 1 : 0], d2 = d[2];
+          const double m4 = (e[i] * dabs(a1[i])) * d2;
+          const double m03 = dmax((e[i] * dabs(a0[i])) * dk, (dabs(a1[i]) * e[i]) * d2);
+          et[i] = 1.0 / sqrt(limit_scaling(i == 4 ? m4 : m03));
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          e[i] = e[i] * et[i];
+          Ec[5 * f + i] = e[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const double qj = dtv[i] * sm.q[3 * f + i];
+          sm.q[3 * f + i] = qj;
+          d[i] = d[i] * dtv[i];
+          Dc[3 * f + i] = d[i];
+          s0 += (c_s * d[i]) * cz[i];
+          qm = dmax(qm, dabs(qj));
+          dm = dmax(dm, d[i]);
+        }
+        acol3(e, mc);  // the next pass's A~ norms
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const double den = d[i] * cz[i];
+          rmin = fmin(rmin, den > 0.0 ? (mc[i] * d[i]) / den : INFINITY);
+        }
+      }
+      {  // one block reduction; partials double-buffered by pass parity (no second barrier)
+        s0 = wave_sum(s0);
+        qm = wave_max(qm);
+        dm = wave_max(dm);
+        rmin = -wave_max(-rmin);
+        double* pr = sm.red4[pass & 1];
+        if ((t & 63) == 0) {
+          pr[4 * (t >> 6) + 0] = s0;
+          pr[4 * (t >> 6) + 1] = qm;
+          pr[4 * (t >> 6) + 2] = dm;
+          pr[4 * (t >> 6) + 3] = rmin;
+        }
+        __syncthreads();
+        s0 = pr[0];
+        qm = pr[1];
+        dm = pr[2];
+        rmin = pr[3];
+#pragma unroll
+        for (int w = 1; w < SC::NWS; ++w) {
+          s0 += pr[4 * w];
+          qm = dmax(qm, pr[4 * w + 1]);
+          dm = dmax(dm, pr[4 * w + 2]);
+          rmin = fmin(rmin, pr[4 * w + 3]);
+        }
+      }
+      const double inf_norm_q = limit_scaling(qm);
+      const double c_temp = 1. / limit_scaling(inf_norm_q);
+      const double c_new = c_s * c_temp;
+      const bool ok1 = ((dm * s0) * M1) / n <= inf_norm_q;
+      const bool ok2 = pass + 1 == p.scaling || (c_new * dm) * M2 <= rmin;
+      if (!(ok1 && ok2)) {  // (block-uniform)
+        resume = true;
+        break;
+      }
+      if (t < NF) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) sm.q[3 * t + i] *= c_temp;
+      }
+      c_s = c_new;
+      dmax_prev = dm;
     }
-    double dmx = 0.0;
-    if (lead && j0 < n) {
-      sm.q[j0] = dtv * sm.q[j0];
-      Dn[j0] = Dc[j0] * dtv;
-      dmx = Dn[j0];
+  }
+  // exact passes: H's columns regenerated for the norms
+  for (; pass < p.scaling; ++pass) {
+    if (!resume) {
+      if (pass == 1) SC_MARK(4);
+      // new scaling factors from the current D, E (every thread reads before anyone writes)
+      double dtv = 1.0;
+      if (lead && j0 < n) {
+        const double pc = (c_s * Dc[j0]) * cm;
+        dtv = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j0))));
+      }
+      double et[SC::RPT];
+#pragma unroll
+      for (int rr = 0; rr < SC::RPT; ++rr) {
+        const int r = t + NTS * rr;
+        et[rr] = r < m ? 1.0 / sqrt(limit_scaling(arow(r))) : 1.0;
+      }
+      double* const Dn = Dc == sm.D[0] ? sm.D[1] : sm.D[0];
+      double* const En = Ec == sm.E[0] ? sm.E[1] : sm.E[0];
+#pragma unroll
+      for (int rr = 0; rr < SC::RPT; ++rr) {
+        const int r = t + NTS * rr;
+        if (r < m) En[r] = Ec[r] * et[rr];
+      }
+      if (lead && j0 < n) {
+        sm.q[j0] = dtv * sm.q[j0];
+        Dn[j0] = Dc[j0] * dtv;
+      }
+      Dc = Dn;
+      Ec = En;
     }
-    dmx = wave_max(dmx);
-    if ((t & 63) == 0) sm.dmx[t >> 6] = dmx;
+    resume = false;
     __syncthreads();
-    Dc = Dn;
-    Ec = En;
-    double dmax_all = sm.dmx[0];
-#pragma unroll
-    for (int w = 1; w < SC::NWS; ++w) dmax_all = fmax(dmax_all, sm.dmx[w]);
-    const double ub = dmax_all * cm0;  // >= this pass's column norm of the D-scaled P
-    double c_temp;
-    bool exact;
-    {
-      double sv = 0.0, qv = 0.0;
-      if (lead && j0 < n) {
-        sv = (c_s * Dc[j0]) * ub;
-        qv = dabs(sm.q[j0]);
-      }
-      block_sum_max<SC::NWS>(sv, qv, sm.redb);
-      const double inf_norm_q = limit_scaling(qv);
-      exact = !(sv / n <= inf_norm_q);  // (block-uniform)
-      c_temp = 1. / limit_scaling(inf_norm_q);
-      if (pass + 1 < p.scaling) {  // the next pass's dtv: c_new D_j ub_j <= |A~ col j| everywhere?
-        const bool bad = !exact && lead && j0 < n && !(((c_s * c_temp) * Dc[j0]) * ub <= acol(j0));
-        exact = __syncthreads_or(exact || bad) != 0;
-      }
+    cm = colmax(false);  // column norms of the D-scaled P (cost normalization)
+    double sv = 0.0, qv = 0.0;
+    if (lead && j0 < n) {
+      sv = (c_s * Dc[j0]) * cm;
+      qv = dabs(sm.q[j0]);
     }
-    if (exact) {
-      cm = colmax(false);  // column norms of the D-scaled P (cost normalization)
-      double sv = 0.0, qv = 0.0;
-      if (lead && j0 < n) {
-        sv = (c_s * Dc[j0]) * cm;
-        qv = dabs(sm.q[j0]);
-      }
-      block_sum_max<SC::NWS>(sv, qv, sm.red);
-      c_temp = sv / n;
-      const double inf_norm_q = limit_scaling(qv);
-      c_temp = dmax(c_temp, inf_norm_q);
-      c_temp = limit_scaling(c_temp);
-      c_temp = 1. / c_temp;
-    } else {
-      cm = ub;  // the next pass's fmax picks the A~ norm either way
-    }
+    block_sum_max<SC::NWS>(sv, qv, sm.red);
+    double c_temp = sv / n;
+    const double inf_norm_q = limit_scaling(qv);
+    c_temp = dmax(c_temp, inf_norm_q);
+    c_temp = limit_scaling(c_temp);
+    c_temp = 1. / c_temp;
     if (lead && j0 < n) sm.q[j0] *= c_temp;  // own column only: no barrier before the next pass
     c_s *= c_temp;
   }

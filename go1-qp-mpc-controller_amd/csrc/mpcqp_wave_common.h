@@ -50,7 +50,7 @@ struct SchurLds;
 // families would leave room for only two robots per CU) the chains apply A and B_k K_k separately,
 // and the R'_k foot blocks share G_k^-1's slot (read by factorization step k before it writes G_k^-1).
 #ifndef MPCQP_ACL_MAXN
-#define MPCQP_ACL_MAXN 20
+#define MPCQP_ACL_MAXN 12
 #endif
 template <int N, bool SACL>
 struct RicFactors;
@@ -594,10 +594,15 @@ struct ScaleImg {
 template <int N>
 struct ScaleCfg {
   static constexpr int n = ND * N, m = CD * N;
+  // Columns of H cached in registers across the passes (off: since the bound-decided passes, H is
+  // generated once per robot, and without the cache four robots fit a CU at N = 10)
+#ifndef MPCQP_SCALE_HREG_MAXN
+#define MPCQP_SCALE_HREG_MAXN 0
+#endif
+  static constexpr bool HREG = N <= MPCQP_SCALE_HREG_MAXN;
 #ifndef MPCQP_SCALE_TPC
 #define MPCQP_SCALE_TPC 2
 #endif
-  static constexpr bool HREG = N <= 10;              // the thread's entries cached in registers
 #ifndef MPCQP_SCALE_TPC_LONG
 #define MPCQP_SCALE_TPC_LONG 1
 #endif
@@ -605,10 +610,12 @@ struct ScaleCfg {
   static constexpr int BPT = (N + TPC - 1) / TPC;    // horizon blocks of the column per thread
   static constexpr int NTS = ((TPC * n + 63) / 64) * 64;
   static constexpr int NWS = NTS / 64;
+  // waves per SIMD the register allocation must allow (launch bounds): N = 10, two waves per robot,
+  // four robots per CU; N = 20, four waves per robot, three per CU (measured, profiles/r04/occ)
 #ifdef MPCQP_SCALE_WPE
   static constexpr int WPE = MPCQP_SCALE_WPE;
 #else
-  static constexpr int WPE = NWS >= 2 ? NWS / 2 : 1;  // waves per SIMD for two robots per CU
+  static constexpr int WPE = N <= 10 ? 2 : 3;
 #endif
   static constexpr int RPT = (m + NTS - 1) / NTS;   // constraint rows per thread
 };
@@ -623,8 +630,8 @@ struct ScaleSmem {
   double vec[2][16];
   double Ap[2][C::m];
   double red[2][16];
-  double redb[2][16];  // the bound test's sums (a buffer of its own: no barrier against red's reads)
-  double dmx[16];      // per-wave max of the new D
+  double cm0[C::n];      // raw column norms of H (the first pass, D = 1)
+  double red4[2][4 * 16];  // bound passes: per-wave partials, double-buffered by pass parity
 };
 
 // block-wide sum of sv and max of qv in one barrier (wave partials summed in wave order)

@@ -14,6 +14,7 @@ import csv, json, sys
 o, b = sys.argv[1], sys.argv[2]
 d = json.load(open(f"{o}/{b}.json"))
 ks = {r["Name"].split("(")[0].split("::")[-1]: float(r["AverageNs"]) / 1e3 for r in csv.DictReader(open(f"{o}/{b}/run_kernel_stats.csv"))}
-print(b, "QP/s", round(d["value"]), "parity", d["parity"]["iters_equal_frac"], d["parity"]["max_rel_err_u0"], {k: round(v, 1) for k, v in ks.items() if "kernel" in k})
+pa = d.get("parity") or {}
+print(b, "QP/s", round(d["value"]), "parity", pa.get("iters_equal_frac"), pa.get("max_rel_err_u0"), {k: round(v, 1) for k, v in ks.items() if "kernel" in k})
 PY
 done
