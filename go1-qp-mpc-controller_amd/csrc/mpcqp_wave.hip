@@ -413,14 +413,27 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
         for (int i = 0; i < 3; ++i) {
           const double cmj = pass == 0 ? cz[i] : dmax_prev * cz[i];
           const double pc = (c_s * d[i]) * cmj;
-          dtv[i] = 1.0 / sqrt(limit_scaling(fmax(pc, mc[i] * d[i])));
+          dtv[i] = limit_scaling(fmax(pc, mc[i] * d[i]));
         }
 #pragma unroll
         for (int i = 0; i < 5; ++i) {  // arow above
           const double dk = d[i < 4 ? i >> 1 : 0], d2 = d[2];
           const double m4 = (e[i] * dabs(a1[i])) * d2;
           const double m03 = dmax((e[i] * dabs(a0[i])) * dk, (dabs(a1[i]) * e[i]) * d2);
-          et[i] = 1.0 / sqrt(limit_scaling(i == 4 ? m4 : m03));
+          et[i] = limit_scaling(i == 4 ? m4 : m03);
+        }
+        // 1 / sqrt of the limited norms; 1 / sqrt(1) = 1 exactly, and on the Go1 workloads every
+        // norm is 1 (unit friction-pyramid entries, D = E = 1): the wave skips the divisions then
+        bool ne1 = false;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) ne1 |= dtv[i] != 1.0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) ne1 |= et[i] != 1.0;
+        if (__any(ne1)) {
+#pragma unroll
+          for (int i = 0; i < 3; ++i) dtv[i] = 1.0 / sqrt(dtv[i]);
+#pragma unroll
+          for (int i = 0; i < 5; ++i) et[i] = 1.0 / sqrt(et[i]);
         }
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
@@ -898,6 +911,15 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
       CAX[e] = sv && si < 6 ? A.at(si, 6 + e) : 0.0;
     }
   }
+  // the LDS address of element c of the lane's row of the packed G_k^-1 in round 0 (step ig)
+  unsigned GADR[NOACL ? 12 : 1];
+  if constexpr (NOACL) {
+    const unsigned gb = lds_off(&sm.u.f.Gp[0][0]) + (unsigned)(sizeof(double) * GPS * ig);
+#pragma unroll
+    for (int e = 0; e < 12; ++e)
+      GADR[e] = gb + (unsigned)sizeof(double) * (unsigned)(e >= idx ? poff(idx) + e - idx : poff(e) + idx - e);
+  }
+  (void)GADR;
   (void)CAT;
   (void)CAX;
   // KS = 1: the lane's rows of R'^-1 (mpcqp_schur.h), set per rho
@@ -1046,13 +1068,20 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
         });
       }
       if (tm_it) WV_MARK(42);
-      // g_k = G_k^-1 t_k
+      // g_k = G_k^-1 t_k: row idx of the packed upper triangle, element c at (min, max) of (idx, c);
+      // per-lane LDS addresses (constant) plus the round's compile-time offset
       {
+        using lds_d = __attribute__((address_space(3))) const double;
         double c0[12], c1[12];
-        ld12(c0, &F.Gi[kc[0]][mo(idx)]);
+        auto ldg = [&](int r, double (&c)[12]) __attribute__((always_inline)) {
+#pragma unroll
+          for (int e = 0; e < 12; ++e)
+            c[e] = *(lds_d*)(GADR[e] + (unsigned)(sizeof(double) * GPS * 4 * r));
+        };
+        ldg(0, c0);
         sfor<0, R>([&](auto RR) {
           constexpr int r = decltype(RR)::value;
-          if constexpr (r + 1 < R) ld12((r & 1) ? c0 : c1, &F.Gi[kc[r + 1]][mo(idx)]);
+          if constexpr (r + 1 < R) ldg(r + 1, (r & 1) ? c0 : c1);
           G[r] = mv12(TT[r], (r & 1) ? c1 : c0);
         });
       }

@@ -65,13 +65,20 @@ struct RicFactors<N, true> {
   double Rt[N][4][6];  // R'_k foot blocks, upper triangle (00 01 02 11 12 22)
   __device__ double* rt(int k) { return &Rt[k][0][0]; }
 };
+// Without Acl, G_k^-1 (symmetric) is kept as its upper triangle, rows packed (row r at poff(r)),
+// GPS doubles per step and 4R steps (whole register rounds, so that every lane's row can be read
+// at a compile-time offset from a per-lane base): the three families then need 40.7 KB at N = 20,
+// four robots per CU.
+__host__ __device__ constexpr int poff(int r) { return 12 * r - r * (r - 1) / 2; }
+constexpr int GPS = 80;
+static_assert(poff(11) + 1 <= GPS, "packed 12 x 12 upper triangle");
 template <int N>
 struct RicFactors<N, false> {
   static constexpr bool HAS_ACL = false;
   static constexpr int NK = N > 1 ? N - 1 : 1;
-  alignas(16) double Gi[N][MS];
+  alignas(16) double Gp[4 * ((N + 3) / 4)][GPS];
   alignas(16) double K[NK][MS];
-  __device__ double* rt(int k) { return &Gi[k][0]; }
+  __device__ double* rt(int k) { return &Gp[k][0]; }
 };
 template <int N, int KS>
 struct WSmem {
@@ -545,9 +552,17 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
     const mf4 Fm = mfma_chain<1, 3>(Bk, PA, zero);  // F = B' P A
     const mf4 Pq = mfma_chain<0, 3>(Ad, PA, cQ);    // cQ + A'P A
     gj_inverse12(G);
-    if (j < 12)
+    if constexpr (std::remove_reference_t<decltype(F)>::HAS_ACL) {
+      if (j < 12)
 #pragma unroll
-      for (int v = 0; v < 3; ++v) F.Gi[k][mo(4 * v + grp) + j] = G[v];
+        for (int v = 0; v < 3; ++v) F.Gi[k][mo(4 * v + grp) + j] = G[v];
+    } else {
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {  // upper triangle (row <= column), rows packed
+        const int row = 4 * v + grp;
+        if (j < 12 && row <= j) F.Gp[k][poff(row) + j - row] = G[v];
+      }
+    }
     if (k >= 1) {
       const mf4 K = mfma_chain<0, 3>(G, Fm, zero);          // K = G^-1 F
       if (j < 12)
