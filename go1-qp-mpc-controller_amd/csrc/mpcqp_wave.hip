@@ -383,7 +383,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     double dmax_prev = 1.0;                           // Dmax of the previous pass (ub_j = Dmax cm0_j)
     for (; pass < p.scaling; ++pass) {
       if (pass == 1) SC_MARK(4);
-      double s0 = 0.0, qm = 0.0, dm = 0.0, rmin = INFINITY;
+      double s0 = 0.0, qm = 0.0, dm = 0.0, rmin = INFINITY, moved = 0.0;
       if (t < NF) {
         const int f = t;
         double e[5], a0[5], a1[5], d[3], cz[3];
@@ -435,6 +435,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
 #pragma unroll
           for (int i = 0; i < 5; ++i) et[i] = 1.0 / sqrt(et[i]);
         }
+        moved = ne1 ? 1.0 : 0.0;
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
           e[i] = e[i] * et[i];
@@ -462,24 +463,28 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
         qm = wave_max(qm);
         dm = wave_max(dm);
         rmin = -wave_max(-rmin);
+        moved = wave_max(moved);
         double* pr = sm.red4[pass & 1];
         if ((t & 63) == 0) {
-          pr[4 * (t >> 6) + 0] = s0;
-          pr[4 * (t >> 6) + 1] = qm;
-          pr[4 * (t >> 6) + 2] = dm;
-          pr[4 * (t >> 6) + 3] = rmin;
+          pr[5 * (t >> 6) + 0] = s0;
+          pr[5 * (t >> 6) + 1] = qm;
+          pr[5 * (t >> 6) + 2] = dm;
+          pr[5 * (t >> 6) + 3] = rmin;
+          pr[5 * (t >> 6) + 4] = moved;
         }
         __syncthreads();
         s0 = pr[0];
         qm = pr[1];
         dm = pr[2];
         rmin = pr[3];
+        moved = pr[4];
 #pragma unroll
         for (int w = 1; w < SC::NWS; ++w) {
-          s0 += pr[4 * w];
-          qm = dmax(qm, pr[4 * w + 1]);
-          dm = dmax(dm, pr[4 * w + 2]);
-          rmin = fmin(rmin, pr[4 * w + 3]);
+          s0 += pr[5 * w];
+          qm = dmax(qm, pr[5 * w + 1]);
+          dm = dmax(dm, pr[5 * w + 2]);
+          rmin = fmin(rmin, pr[5 * w + 3]);
+          moved = dmax(moved, pr[5 * w + 4]);
         }
       }
       const double inf_norm_q = limit_scaling(qm);
@@ -495,8 +500,16 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
 #pragma unroll
         for (int i = 0; i < 3; ++i) sm.q[3 * t + i] *= c_temp;
       }
+      // A pass that moved nothing (every 1/sqrt factor 1, c_temp 1, the same Dmax) leaves the next
+      // pass exactly the same inputs: every remaining pass is the identity.  (Go1 workloads: from
+      // the second or third pass on.)
+      const bool fixed = moved == 0.0 && c_temp == 1.0 && dm == dmax_prev;
       c_s = c_new;
       dmax_prev = dm;
+      if (fixed) {
+        pass = p.scaling;
+        break;
+      }
     }
   }
   // exact passes: H's columns regenerated for the norms

@@ -646,7 +646,7 @@ struct ScaleSmem {
   double Ap[2][C::m];
   double red[2][16];
   double cm0[C::n];      // raw column norms of H (the first pass, D = 1)
-  double red4[2][4 * 16];  // bound passes: per-wave partials, double-buffered by pass parity
+  double red4[2][5 * 16];  // bound passes: per-wave partials, double-buffered by pass parity
 };
 
 // block-wide sum of sv and max of qv in one barrier (wave partials summed in wave order)
