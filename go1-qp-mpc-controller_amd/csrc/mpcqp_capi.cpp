@@ -6,7 +6,6 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
-#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -23,9 +22,7 @@ struct mpcqp_handle {
   double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
   size_t work_per = 0;       // doubles per instance the workspace was sized for
-  int* fb = nullptr;         // wave path: fallback list + time-slicing queue, fallback_ints(work_cap)
-  double* slice = nullptr;   // wave path, Schur form: per-robot slice save areas [work_cap]
-  int slice_iters = mpcqp::SLICE_ITERS;  // iterations per slice (MPCQP_SLICE overrides; 0 = off)
+  int* fb = nullptr;         // wave path: Schur -> Riccati fallback list [work_cap + 1] ints
   int path = 0;              // 0 auto (= 3), 3 Riccati wave; debug library only: 1 dense K^-1, 2 Riccati workgroup
   // host wrapper: device buffers, a private stream and two pinned staging chunks
   hipStream_t hstream = nullptr;
@@ -108,17 +105,13 @@ hipError_t ensure_workspace(mpcqp_handle* h, int32_t batch, void* stream) {
   hipError_t e = hipStreamSynchronize((hipStream_t)stream);
   if (e == hipSuccess) e = hipFree(h->work);
   if (e == hipSuccess) e = hipFree(h->fb);
-  if (e == hipSuccess) e = hipFree(h->slice);
   h->work = nullptr;
   h->fb = nullptr;
-  h->slice = nullptr;
   const size_t cap = (size_t)batch > h->work_cap ? (size_t)batch : h->work_cap;
   h->work_cap = 0;
   h->work_per = 0;
   if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * per * cap);
-  if (e == hipSuccess) e = hipMalloc(&h->fb, sizeof(int) * mpcqp::fallback_ints(cap));
-  const size_t sper = effective_path(h) == 3 ? mpcqp::slice_state_doubles_any(h->p) : 0;
-  if (e == hipSuccess && sper > 0) e = hipMalloc(&h->slice, sizeof(double) * sper * cap);
+  if (e == hipSuccess) e = hipMalloc(&h->fb, sizeof(int) * (cap + 1));
   if (e == hipSuccess) {
     h->work_cap = cap;
     h->work_per = per;
@@ -250,7 +243,6 @@ int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** 
   if (per_cu < 1) per_cu = 1;
   h->slots = cus * per_cu;
   h->cus = cus;
-  if (const char* sl = getenv("MPCQP_SLICE")) h->slice_iters = atoi(sl);  // (tuning experiments)
   *out = h;
   return MPCQP_OK;
 }
@@ -260,7 +252,6 @@ int32_t mpcqp_destroy(mpcqp_handle* h) {
   DeviceGuard dg(h->device);
   (void)hipFree(h->work);
   (void)hipFree(h->fb);
-  (void)hipFree(h->slice);
   (void)hipFree(h->d_recs);
   (void)hipFree(h->d_res);
   (void)hipFree(h->d_sol);
@@ -298,9 +289,7 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   a.trace_cap = d_trace ? trace_cap : 0;
   a.wstate = d_state;
   a.fallback = h->fb;
-  a.slice_state = h->slice;
-  a.slice = h->slice_iters;
-  a.grid = effective_path(h) == 3 ? h->slots : batch;  // (wave path: the persistent grid when it slices)
+  a.grid = batch;
   a.stream = stream;
   a.p = h->p;
   switch (effective_path(h)) {

@@ -18,10 +18,7 @@ struct LaunchArgs {
   double* trace;
   int trace_cap;
   double* wstate;  // warm-start slots [batch][warm_state_doubles(N)] (wave path) or nullptr
-  int* fallback;   // wave path: fallback_ints(batch) ints (handle-owned): the Schur -> Riccati
-                   // fallback list, then the time-slicing queue (see wave_kernel)
-  double* slice_state = nullptr;  // wave path, Schur form: per-robot state saved between slices
-  int slice = 0;                  // iterations per slice (0: every robot runs to the end in one go)
+  int* fallback;   // wave path: [batch + 1] ints, the Schur -> Riccati fallback list (handle-owned)
   int grid;
   void* stream;
   mpcqp_params p;
@@ -36,15 +33,6 @@ hipError_t launch_wave_any(const LaunchArgs& a);
 hipError_t occupancy_wave_any(const mpcqp_params& p, int* blocks);
 // grid of the Riccati fallback launch after the Schur-form wave kernel (grid-stride over its list)
 constexpr int FALLBACK_GRID = 1024;
-// Time slicing of the Schur-form wave kernel: continuations the queue can hold per robot, and the
-// ints of the handle's list buffer: [1 + batch] fallback list, [4] queue counters (pop, push,
-// finished), [batch * SLICE_QMAX] continuation slots
-constexpr int SLICE_QMAX = 8;
-inline size_t fallback_ints(size_t batch) { return 1 + batch + 4 + batch * SLICE_QMAX; }
-// doubles per robot of the slice save area (0 where the wave path does not slice)
-size_t slice_state_doubles_any(const mpcqp_params& p);
-// iterations per slice of the default solve
-constexpr int SLICE_ITERS = 75;
 hipError_t wave_selftest(double* d_out, void* stream);
 hipError_t launch_scale_any(const LaunchArgs& a);  // scale_kernel alone (the image in a.work)
 constexpr int WAVE_MAX_HORIZON = 20;

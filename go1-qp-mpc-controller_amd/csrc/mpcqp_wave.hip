@@ -67,12 +67,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   const int inst = blockIdx.x;
   if (inst >= batch) return;
   const int t = threadIdx.x;
-  // wave_kernel's fallback list and time-slicing queue start empty (stream order)
-  if (inst == 0 && t < 4) {
-    if (t == 0) fb[0] = 0;
-    fb[1 + batch + t] = 0;
-  }
-  if (t < SLICE_QMAX) fb[1 + batch + 4 + (size_t)inst * SLICE_QMAX + t] = 0;
+  if (inst == 0 && t == 0) fb[0] = 0;  // wave_kernel's fallback list starts empty (stream order)
   {
     const double* rg = recs + (size_t)inst * C::REC;
     int bad = 0;
@@ -618,38 +613,18 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   } while (0)
 #endif
 
-// Time slicing (KS = 1): a robot still running at the first termination check `slice` iterations
-// into its slice saves its loop state and re-queues itself behind every robot already queued, so
-// that the last robots of a batch do not finish alone on a few CUs (round robin over the batch;
-// each robot's arithmetic is unchanged: the restore recomputes only what the loop derives from the
-// saved values).  Save area of one robot: scalars, the lane registers X, Z, Y, Z4, Y4 and the
-// R'^-1 rows (lane-major, coalesced), and the factorization's LDS (Q and B) unless a refactorization
-// is due anyway.
-template <int N>
-struct SliceLayout {
-  static constexpr int R = Cfg<N>::R;
-  static constexpr int SCAL = 16;
-  static constexpr int NARR = 8 * R;  // X, Z, Y, Z4, Y4 and three R'^-1 columns, per round
-  static constexpr int LDS = SCAL + NARR * NT;
-  static constexpr int LDSD = (int)(offsetof(SchurLds<N>, wv) / sizeof(double));
-  static constexpr int SIZE = LDS + LDSD;
-};
-
 // KS: the KKT solve.  0 = Riccati recursion (chains over the horizon, factors on MFMA; every N),
 // 1 = impulse-space Schur form (mpcqp_schur.h; N <= 10, nonnegative state weights).
 // The solve of robot `inst` by one wave (the kernels below: one robot per workgroup, or the
 // Riccati fallback's list of robots).  KS = 1 robots whose G_k is (nearly) singular append
 // themselves to fb (fb[0] = count, fb[1..]) and return without writing anything: the fallback
 // kernel solves them with KS = 0.
-// Returns 1 when the robot yielded (its state saved and its continuation queued), 0 otherwise.
 template <int N, int KS>
-__device__ __forceinline__ int wave_solve(const int inst, WSmem<N, KS>& sm, const double* __restrict__ recs,
-                                          mpcqp_result* __restrict__ results, double* __restrict__ solution,
-                                          double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
-                                          const double* __restrict__ img, const mpcqp_params& p,
-                                          int* __restrict__ fb, double* __restrict__ sv = nullptr,
-                                          bool resume = false, int slice = 0, int* qc = nullptr, int* cq = nullptr,
-                                          int qcap = 0) {
+__device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, const double* __restrict__ recs,
+                                           mpcqp_result* __restrict__ results, double* __restrict__ solution,
+                                           double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
+                                           const double* __restrict__ img, const mpcqp_params& p,
+                                           int* __restrict__ fb) {
   using C = Cfg<N>;
   using WL = WarmLayout<N>;
   constexpr int n = C::n, m = C::m, R = C::R;
@@ -683,7 +658,7 @@ __device__ __forceinline__ int wave_solve(const int inst, WSmem<N, KS>& sm, cons
       }
       if (solution)
         for (int e = t; e < n; e += NT) solution[(size_t)inst * n + e] = NAN;
-      return 0;
+      return;
     }
   }
   wave_sync();
@@ -741,7 +716,7 @@ __device__ __forceinline__ int wave_solve(const int inst, WSmem<N, KS>& sm, cons
       const int j = atomicAdd(fb, 1);
       fb[1 + j] = inst;
     }
-    return 0;
+    return;
   }
   for (int j = t; j < n; j += NT) {
     HS.D[j] = im[SI::D + j];
@@ -984,44 +959,7 @@ __device__ __forceinline__ int wave_solve(const int inst, WSmem<N, KS>& sm, cons
   double obj_sum = 0.0;  // 1/2 x'P~x + q~'x of the final iterate (scaled), set when the loop ends
   bool need_factor = true;
   int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
-  int iter0 = 1;
-  using SL = SliceLayout<N>;
-  if constexpr (KS == 1) {
-    if (resume) {  // the state this robot saved when it yielded (see SliceLayout)
-      iter0 = (int)sv[0];
-      rho = sv[1];
-      pri_res = sv[2];
-      dua_res = sv[3];
-      iters = (int)sv[4];
-      rho_updates = (int)sv[5];
-      to_check = (int)sv[6];
-      to_adapt = (int)sv[7];
-      need_factor = sv[8] != 0.0;
-      rinv = 1. / rho;
-      const double* la = sv + SL::SCAL + t;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        X[r] = la[(0 * R + r) * NT];
-        Z[r] = la[(1 * R + r) * NT];
-        Y[r] = la[(2 * R + r) * NT];
-        Z4[r] = la[(3 * R + r) * NT];
-        Y4[r] = la[(4 * R + r) * NT];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) SRI[r][c] = la[((5 + c) * R + r) * NT];
-        RHO4[r] = rho4_of(r, rho);
-        RI4[r] = 1. / RHO4[r];
-        // the loop's right-hand side of this iterate (update(): every lane)
-        const double at = quad_at(rho * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
-        RHS[r] = (sigma * X[r] - Qv[r]) + at;
-      }
-      if (!need_factor) {
-        double* fl = reinterpret_cast<double*>(&F);
-        for (int e = t; e < SL::LDSD; e += NT) fl[e] = sv[SL::LDS + e];
-        wave_sync();
-      }
-    }
-  }
-  for (int iter = iter0; iter <= p.max_iter; ++iter) {
+  for (int iter = 1; iter <= p.max_iter; ++iter) {
     if (need_factor) {
 #ifdef MPCQP_REPEAT_FACTOR  // cost measurement builds: the (idempotent) factorization runs twice
      for (int rep = 0; rep < 2; ++rep) {
@@ -1612,46 +1550,6 @@ __device__ __forceinline__ int wave_solve(const int inst, WSmem<N, KS>& sm, cons
           RHS[r] = (sigma * X[r] - Qv[r]) + at;
         }
       }
-      if constexpr (KS == 1) {
-        // end of the slice: save, then queue the continuation (when the queue has room)
-        if (slice > 0 && is_check && iter - iter0 + 1 >= slice) {
-          int j = 0;
-          if (t == 0) j = atomicAdd(&qc[1], 1);
-          j = __builtin_amdgcn_readfirstlane(__shfl(j, 0));
-          if (j < qcap) {
-            if (t == 0) {
-              sv[0] = iter + 1;
-              sv[1] = rho;
-              sv[2] = pri_res;
-              sv[3] = dua_res;
-              sv[4] = iters;
-              sv[5] = rho_updates;
-              sv[6] = to_check;
-              sv[7] = to_adapt;
-              sv[8] = need_factor ? 1.0 : 0.0;
-            }
-            double* la = sv + SL::SCAL + t;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-              la[(0 * R + r) * NT] = X[r];
-              la[(1 * R + r) * NT] = Z[r];
-              la[(2 * R + r) * NT] = Y[r];
-              la[(3 * R + r) * NT] = Z4[r];
-              la[(4 * R + r) * NT] = Y4[r];
-#pragma unroll
-              for (int c = 0; c < 3; ++c) la[((5 + c) * R + r) * NT] = SRI[r][c];
-            }
-            if (!need_factor) {
-              const double* fl = reinterpret_cast<const double*>(&F);
-              for (int e = t; e < SL::LDSD; e += NT) sv[SL::LDS + e] = fl[e];
-            }
-            __threadfence();  // the saved state is visible before the continuation is
-            wave_sync();
-            if (t == 0) __hip_atomic_store(&cq[j], inst + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            return 1;
-          }
-        }
-      }
     }
     if (tm_ck) WV_MARK(49);
     if (tm_it) WV_MARK(47);
@@ -1739,21 +1637,6 @@ __device__ __forceinline__ int wave_solve(const int inst, WSmem<N, KS>& sm, cons
     res->iters = iters;
     res->rho_updates = rho_updates;
   }
-  return 0;
-}
-
-// The Schur-form solve of one robot (slice) as a function of its own: inlined into the kernel's
-// queue loop, its loop-invariant values were hoisted out of the robot loop and spilled (~140 VGPRs
-// of scratch traffic); called, it is allocated like the one-robot-per-workgroup kernel.
-template <int N>
-__device__ __noinline__ int wave_solve_slice(const int inst, WSmem<N, 1>& sm, const double* __restrict__ recs,
-                                             mpcqp_result* __restrict__ results, double* __restrict__ solution,
-                                             double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
-                                             const double* __restrict__ img, const mpcqp_params& p,
-                                             int* __restrict__ fb, double* __restrict__ sv, bool resume, int slice,
-                                             int* qc, int* cq, int qcap) {
-  return wave_solve<N, 1>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb, sv, resume, slice,
-                          qc, cq, qcap);
 }
 
 template <int N, int KS>
@@ -1762,53 +1645,11 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                                                      double* __restrict__ solution, double* __restrict__ trace,
                                                      int trace_cap, double* __restrict__ wstate,
                                                      const double* __restrict__ img, mpcqp_params p,
-                                                     int* __restrict__ fb, double* __restrict__ slice_state,
-                                                     int slice) {
+                                                     int* __restrict__ fb) {
   __shared__ WSmem<N, KS> sm;
-  if constexpr (KS == 1) {
-    {
-      // Workgroups over a queue: pop index i < batch is robot i's first slice, i >= batch the
-      // (i - batch)-th continuation pushed (wait until it is published, or until every robot has
-      // finished; without slicing nothing is ever pushed).  Every wave exits: a wait ends with a
-      // publication or with the last finish.
-      int* qc = fb + 1 + batch;  // [0] pops, [1] pushes, [2] robots finished
-      int* cq = qc + 4;          // continuations: robot + 1, published with release
-      const int qcap = slice > 0 ? batch * SLICE_QMAX : 0;
-      for (;;) {
-        int item = -1;
-        if (threadIdx.x == 0) {
-          const int i = atomicAdd(&qc[0], 1);
-          if (i < batch) {
-            item = i;
-          } else if (i - batch < qcap) {
-            const int j = i - batch;
-            for (;;) {
-              const int v = __hip_atomic_load(&cq[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-              if (v != 0) {
-                item = (v - 1) | (1 << 30);
-                break;
-              }
-              if (__hip_atomic_load(&qc[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= batch) break;
-              __builtin_amdgcn_s_sleep(4);
-            }
-          }
-        }
-        item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));  // (wave-uniform: scalar addressing)
-        if (item < 0) break;
-        const int inst = item & ((1 << 30) - 1);
-        const bool resume = (item >> 30) & 1;
-        const int y = wave_solve_slice<N>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb,
-                                          slice_state + (size_t)inst * SliceLayout<N>::SIZE, resume, slice, qc, cq,
-                                          qcap);
-        wave_sync();
-        if (y == 0 && threadIdx.x == 0) atomicAdd(&qc[2], 1);
-      }
-    }
-  } else {
-    const int inst = blockIdx.x;
-    if (inst >= batch) return;
-    wave_solve<N, KS>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb);
-  }
+  const int inst = blockIdx.x;
+  if (inst >= batch) return;
+  wave_solve<N, KS>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb);
 }
 
 // The robots wave_kernel<N, 1> handed over (fb[0] of them at fb[1..]), by the Riccati form; a
@@ -1865,12 +1706,8 @@ static hipError_t launch_wave(const LaunchArgs& a) {
   if (e != hipSuccess) return e;
   if constexpr (N <= 10) {
     if (schur_ok(a.p)) {
-      // time slicing on persistent workgroups (not with the debug trace, whose records are per slice)
-      const bool sl = a.slice > 0 && a.slice_state && !a.trace && a.grid > 0;
-      const int wgrid = sl ? (a.batch < a.grid ? a.batch : a.grid) : a.batch;
-      hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(wgrid), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs,
-                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback,
-                         a.slice_state, sl ? a.slice : 0);
+      hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs,
+                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
       e = hipGetLastError();
       if (e != hipSuccess) return e;
       // the robots with (nearly) singular G_k, if any (an empty list costs one short launch)
@@ -1881,14 +1718,8 @@ static hipError_t launch_wave(const LaunchArgs& a) {
     }
   }
   hipLaunchKernelGGL((wv::wave_kernel<N, 0>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs, a.batch,
-                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback, nullptr, 0);
+                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
   return hipGetLastError();
-}
-template <int N>
-static size_t slice_state_doubles(const mpcqp_params& p) {
-  if constexpr (N <= 10)
-    if (schur_ok(p)) return wv::SliceLayout<N>::SIZE;
-  return 0;
 }
 template <int N>
 static hipError_t launch_scale(const LaunchArgs& a) {
@@ -1935,15 +1766,6 @@ hipError_t occupancy_wave_any(const mpcqp_params& p, int* blocks) {
     MPCQP_WAVE_FOR_EACH_N(CASE)
 #undef CASE
     default: return hipErrorInvalidValue;
-  }
-}
-size_t slice_state_doubles_any(const mpcqp_params& p) {
-  switch (p.horizon) {
-#define CASE(K) \
-  case K: return slice_state_doubles<K>(p);
-    MPCQP_WAVE_FOR_EACH_N(CASE)
-#undef CASE
-    default: return 0;
   }
 }
 hipError_t wave_selftest(double* d_out, void* stream) {
