@@ -88,16 +88,20 @@ def test_scale_image_matches_oracle_on_bench_samples(oracle, cfg):
     _check_cold(oracle, recs[idx], 10, label=cfg)
 
 
-def test_scale_image_warm_branches_match_oracle(oracle):
+@pytest.mark.parametrize("heavy", [False, True], ids=["go1_weights", "heavy_weights"])
+def test_scale_image_warm_branches_match_oracle(oracle, heavy):
     """Warm slots: per tick the branch (update_P vs re-init) and the scaled data the warm solve starts
     from (after update_P or re-init, q~ = c (D q) of this tick's gradient: osqp_update_lin_cost, the
-    expression wave_kernel applies to the image's raw gradient)."""
+    expression wave_kernel applies to the image's raw gradient).  heavy: weights x1e4, so that the
+    osqp_update_P branch's Ruiz passes (on the previous tick's A) also run exact passes."""
     T, B, N = 6, 24, 10
     ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=23, gait="trot", swing_ticks=3)
     recs_t = np.stack([mpcqp.assemble_compute_grf(s, N) for s in ticks])
     recs_t[3:, ::3, mpcqp._lib.REC_MU] = 0.5  # a friction change: OsqpEigen re-init for those robots
-    p = mpcqp.default_params(N)
-    op = oracle.default_params(N)
+    p0 = mpcqp.default_params(N)
+    kw = {"q_weights": [w * 1e4 for w in p0.q_weights], "r_weights": [w * 1e4 for w in p0.r_weights]} if heavy else {}
+    p = mpcqp.default_params(N, **kw)
+    op = oracle.default_params(N, q=list(p.q_weights), r=list(p.r_weights))
     ws = [oracle.WarmSolver(op) for _ in range(B)]
     modes = set()
     with mpcqp.MpcQpSolver(p, debug=True) as s:
