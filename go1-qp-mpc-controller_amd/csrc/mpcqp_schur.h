@@ -169,9 +169,11 @@ __device__ __forceinline__ double alpha_jl(int N, int j, int l) {
 // B in LDS and, per lane, RI[r][3] (row a of R'^-1 of its foot, variable role).
 // (G_k is positive definite for the robots that reach it: scale_kernel screens out rank-deficient
 // B6_k, whose robots the Riccati form solves)
+// smax: max_i S_ii (>= 1; a lower bound on the condition of S, whose eigenvalues are >= 1), from the
+// lanes' own V, W rows: S_ii = 1 + beta_kk |v_i|^2 + alpha_kk |w_i|^2.
 template <int N, int R, class SM, class Mark>
 __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp_params& p, const Adisc& A, double cost_c,
-                             double dtm, double (&RI)[R][3], Mark&& mark) {
+                             double dtm, double (&RI)[R][3], Mark&& mark, double& smax) {
   constexpr int QS = SchurCfg<N>::QS;
   constexpr int NI = SchurCfg<N>::NI;
   auto& sc = F.s;
@@ -331,6 +333,16 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   wave_sync();
   }
 #endif
+  {
+    double sv = 0.0, sw = 0.0;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      sv += vw[e] * vw[e];
+      sw += vw[6 + e] * vw[6 + e];
+    }
+    const double sii = (1.0 + (double)(N - k) * sv) + alpha_jl(N, k, k) * sw;
+    smax = __any(iv && !(sii <= SCHUR_SMAX)) ? 2.0 * SCHUR_SMAX : 1.0;
+  }
   mark(13);
   // S - I = L'CL = beta o (V V') + alpha o (W W') (V, W: the 6-column halves of vw; beta, alpha per
   // step pair), row i in absolute column order, by row_newbcast dot products against four row

@@ -1003,8 +1003,17 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
       wave_sync();
       if constexpr (KS == 0) factorize_mfma<N>(sm, p, A, cost_c, dtm, Q2J);
       else {
+        double smax;
         schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI,
-                           [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; });
+                           [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; }, smax);
+        // The push-through identity subtracts B'(I - S^-1)B w from R'^-1 w: with S ill-conditioned
+        // (large state weights, four feet in contact) the difference loses digits the Riccati form
+        // keeps.  Such a robot leaves the loop at the next need_info iteration (one follows every
+        // factorization before the next one; an exit right here cost 8 % of the kernel in register
+        // allocation) and is handed to the Riccati form (wave_fallback_kernel), which solves it
+        // from the start; nothing of it has been written.  max S_ii of the latest factorization
+        // lives in the robot's image slot, not in a loop-carried register.
+        if (t == 0) const_cast<double*>(im)[SI::DEGEN] = smax;
       }
       wave_sync();
 #ifdef MPCQP_REPEAT_FACTOR
@@ -1518,7 +1527,8 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
       }
       if (tm_ck) WV_MARK(52);
       if (last && st == MPCQP_STATUS_UNSOLVED) st = MPCQP_STATUS_MAX_ITER_REACHED;
-      if (last) done = true;
+      // (an ill-conditioned factorization since the last check: leave now, see the factorization)
+      if (last || (KS == 1 && !(img_at(SI::DEGEN) <= SCHUR_SMAX))) done = true;
       status = st;
 #ifndef MPCQP_PHASE_TIMING
       if (trace && t == 0 && inst < trace_cap && ntrace < MPCQP_TRACE_LEN && is_check) {
@@ -1556,6 +1566,13 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
   }
 
   WV_MARK(20);
+  if (KS == 1 && !(img_at(SI::DEGEN) <= SCHUR_SMAX)) {  // ill-conditioned S: the Riccati form solves it
+    if (t == 0) {
+      const int j = atomicAdd(fb, 1);
+      fb[1 + j] = inst;
+    }
+    return;
+  }
   if (ws) {  // the solver persists: scaling, scaled data, iterates and rho for the next tick
     if (t == 0) {
       ws[WL::FLAG] = 1.0;

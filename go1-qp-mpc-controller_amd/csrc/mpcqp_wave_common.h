@@ -598,6 +598,14 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
 // over columns differs from the single-wave version (a different but equally exact summation).
 // B6_k Gram pivot ratio below which a robot is handed to the Riccati form (scale_kernel's screen)
 constexpr double SCHUR_GRAM_TOL = 1e-6;
+// max_i S_ii above which the Schur form hands a robot to the Riccati form (mpcqp_schur.h).
+// Measured (profiles/r04/smax, tools/fuzz_parity.py): four feet in contact, state weights x 5 /
+// x 100: u0 off the oracle by 4e-4 / 1e-3 without the hand-off, 9e-7 with it at 1e4; no C2 (trot)
+// robot crosses 1e4; a threshold of 1e3 sends most C2 robots to the Riccati form (-35 %)
+#ifndef MPCQP_SCHUR_SMAX
+#define MPCQP_SCHUR_SMAX 1e4
+#endif
+constexpr double SCHUR_SMAX = MPCQP_SCHUR_SMAX;
 template <int N>
 struct ScaleImg {
   static constexpr int n = ND * N, m = CD * N;

@@ -1,0 +1,29 @@
+"""Ill-conditioned Schur cores (mpcqp_schur.h, wave_kernel's hand-off): with four feet in contact
+and state weights a few times the Go1 defaults, S = I + L'CL gets large and the push-through
+identity R'^-1 w - B'(I - S^-1)B w loses digits (u0 off the oracle by up to 1e-3 at x 100, round-4
+fuzz, profiles/r04/smax).  wave_kernel hands robots whose max S_ii exceeds SCHUR_SMAX to the Riccati
+form.  Gates: status and iterations equal to the oracle, u0 within SURVEY §8(c)'s 1e-4."""
+import numpy as np
+import pytest
+
+import mpcqp
+from gpu_helpers import rel_err_u0, solve_gpu
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("scale", [1.0, 5.0, 100.0])
+@pytest.mark.parametrize("gait", ["stance", "mixed"])
+def test_heavy_state_weights_match_oracle(oracle, gait, scale):
+    N, B = 10, 512
+    st = mpcqp.synthetic_go1(B, seed=7000 + 97 * 5 + N, gait=gait, mixed_mu=(gait == "mixed"))
+    recs = mpcqp.assemble_compute_grf(st, N)
+    p0 = mpcqp.default_params(N)
+    p = mpcqp.default_params(N, q_weights=[w * scale for w in p0.q_weights])
+    with mpcqp.MpcQpSolver(p) as s:
+        got, _, _ = solve_gpu(s, recs)
+    ref = oracle.solve_batch(oracle.default_params(N, q=list(p.q_weights), r=list(p.r_weights)), recs, nthreads=8)
+    np.testing.assert_array_equal(got["status"], ref["status"])
+    np.testing.assert_array_equal(got["iters"], ref["iters"])
+    err = rel_err_u0(got["u0"], ref["u0"])
+    assert np.all(err <= 1e-4), float(err.max())
