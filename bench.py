@@ -92,9 +92,13 @@ def parse_args(argv=None):
     ap.add_argument("--mixed-mu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=4096,
                     help="instances timed on the CPU oracle (4096 x ~2.3 ms = ~10 s of CPU work)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, usable cpus)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the e2e / c4 / c5 / warm_tick keys")
+    ap.add_argument("--dist", action="store_true",
+                    help="take the distributed branch (process group, per-step all-gather, allgather_ms, "
+                         "gathered parity) at any world size, --gpus 1 included: a world-1 RCCL run on one "
+                         "GPU exercises the C3 collective path's code before an 8-GPU node does")
     ap.add_argument("--cpu-stub", action="store_true",
                     help="TEST ONLY: gloo backend on the CPU, a deterministic stub in place of the device "
                          "solve (exercises the launcher, sharding and all-gather without a GPU)")
@@ -164,16 +168,17 @@ def run_rank(args):
     from mpcqp.distributed import allgather_forces, env_rank, shard_range
 
     world, rank, local_rank = env_rank()
+    dist_on = world > 1 or args.dist  # the process group and the per-step all-gather (C3 path)
     if args.cpu_stub:
         dev = torch.device("cpu")
-        if world > 1:
+        if dist_on:
             dist.init_process_group("gloo")
     else:
         dev = torch.device("cuda", local_rank)
         torch.cuda.set_device(dev)
-        if world > 1:
+        if dist_on:
             dist.init_process_group("nccl", device_id=dev)
-    ranks_seen = dist.get_world_size() if world > 1 else 1
+    ranks_seen = dist.get_world_size() if dist_on else 1
     if ranks_seen != args.gpus:
         raise SystemExit(f"bench: {ranks_seen} ranks but --gpus {args.gpus}")
 
@@ -213,7 +218,7 @@ def run_rank(args):
                   for _ in range(args.steps)]
         # the all-gather's own span per step (RCCL runs on the current stream; for the gloo stub the
         # host clock around the blocking call)
-        gevents = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if world > 1 else None
+        gevents = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if dist_on else None
     gather_host_s = []
 
     def step(k=None):
@@ -222,7 +227,7 @@ def run_rank(args):
         solve()
         if events is not None and k is not None:
             events[k][1].record(stream)
-        if world > 1:  # the production exchange: u0 of every robot on every rank
+        if dist_on:  # the production exchange: u0 of every robot on every rank
             tg = time.perf_counter()
             full = allgather_forces(d_res[:, :12].contiguous(), total)
             if k is not None:
@@ -236,24 +241,24 @@ def run_rank(args):
     for _ in range(args.warmup):
         step()
     sync()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
         full = step(k)
     sync()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else None
     gather_ms = None
-    if world > 1:
+    if dist_on:
         # solve end -> all-gather end of every timed step (max over ranks below)
         if gevents is not None:
             gather_ms = float(np.mean([events[k][1].elapsed_time(gevents[k]) for k in range(args.steps)]))
@@ -265,7 +270,7 @@ def run_rank(args):
         kern_max_ms = float(gm[1].item())
 
     # whole results of every rank (outside the timed region) for the parity sample
-    if world > 1:
+    if dist_on:
         all_rows = allgather_forces(d_res, total).cpu().numpy()
         u0_full = full.cpu().numpy()
     else:
@@ -290,14 +295,15 @@ def run_rank(args):
                          "gait": args.gait, "parallelism": f"dp{world}", "ranks_seen": ranks_seen,
                          "sharding": "contiguous shard_range of one seeded global batch per rank",
                          "collective": "RCCL all_gather of u0 per step (mpcqp.distributed.allgather_forces)"
-                         if world > 1 else "none"}
-        gather_ok = bool(np.array_equal(u0_full, res_all["u0"])) if world > 1 else True
-        if world > 1:
+                         if dist_on else "none"}
+        gather_ok = bool(np.array_equal(u0_full, res_all["u0"])) if dist_on else True
+        if dist_on:
             out["extras"] = {"allgather_ms": gather_ms, "solve_kernel_ms_max_over_ranks": kern_max_ms,
                              "allgather_what": ("per timed step: end of the rank's solve -> end of the "
                                                 "all-gather of u0 (HIP events on the solve stream; gloo stub: "
                                                 "host clock), mean over steps, max over ranks"),
-                             "allgather_bytes_per_rank": int(Bl * 12 * 8)}
+                             "allgather_bytes_per_rank": int(Bl * 12 * 8),
+                             "backend": dist.get_backend()}
         if args.cpu_stub:
             exp = stub_results(recs_global)
             out["parity"] = {"gather_exact": bool(np.array_equal(u0_full, exp["u0"]) and gather_ok),
@@ -331,7 +337,7 @@ def run_rank(args):
                 out["parity"] = parity_of(res_all[idx], ref)
                 out["parity"]["sample"] = f"{len(idx)} robots evenly spaced over the global batch"
                 out["parity"]["gathered_u0_equals_rank_results"] = gather_ok
-                if world == 1:
+                if not dist_on:
                     out["cpu_baseline"] = cpu_baseline(pyoracle, op, recs_np, args)
             else:
                 out["parity"] = None
@@ -339,18 +345,40 @@ def run_rank(args):
             out["stats"] = {"mean_iters": float(res_all["iters"].mean()), "max_iters": int(res_all["iters"].max()),
                             "mean_rho_updates": float(res_all["rho_updates"].mean()),
                             "solved_frac": float(np.mean(res_all["status"] == 1))}
-            if world == 1 and not args.no_extras:
+            if not dist_on and not args.no_extras:
                 out["extras"] = extras(args, solver, params, recs_np, states, local_res, pyoracle, dev)
     if solver is not None:
         solver.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     return out
 
 
+def host_cpu():
+    """(model name, nproc, CPUs this process may run on) of the host."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, usable
+
+
 def cpu_baseline(pyoracle, op, recs_np, args):
     S = min(args.cpu_sample, recs_np.shape[0])
-    nthr = args.cpu_threads or min(16, os.cpu_count() or 1)
+    model, nproc, usable = host_cpu()
+    # The GPU box allots 16 CPUs per GPU (its harness rule for worker pools; nproc there shows the
+    # whole machine): the timed run uses that share, and the line also gives the all-cores figure
+    # extrapolated from the single-thread rate (robots are independent: linear at best).
+    nthr = args.cpu_threads or min(16, usable)
     pyoracle.solve_batch(op, recs_np[:min(S, 64)], nthreads=nthr)  # warm
     tc = time.perf_counter()
     pyoracle.solve_batch(op, recs_np[:S], nthreads=nthr)
@@ -363,7 +391,11 @@ def cpu_baseline(pyoracle, op, recs_np, args):
             "sample": f"first {S} instances of this workload (same seed) on oracle/mpc_oracle.c "
                       f"(binary64 ConvexMpc + OSQP-0.6 restatement), {nthr} host threads; "
                       f"single-thread {t1 * 1e6:.0f} us/QP",
-            "single_thread_us_per_qp": t1 * 1e6}
+            "single_thread_us_per_qp": t1 * 1e6, "cpu_model": model, "nproc": nproc,
+            "cpus_usable": usable, "threads_used": nthr,
+            "all_cores_extrapolated_value": nproc / t1,
+            "all_cores_note": "nproc x the single-thread rate (perfect scaling assumed; an upper bound "
+                              "on the whole host, not measured: the box allots 16 CPUs per GPU)"}
 
 
 def _timed(fn, steps, stream):
@@ -587,7 +619,7 @@ def extras(args, solver, params, recs_np, states, base_res, pyoracle, dev):
 def main(argv=None):
     args = parse_args(argv)
     from mpcqp.distributed import env_rank, launch_ranks
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if (args.gpus > 1 or args.dist) and "WORLD_SIZE" not in os.environ:
         # launcher: this process never touches the GPU; the ranks each open their own device
         return launch_ranks(os.path.abspath(__file__), sys.argv[1:] if argv is None else argv, args.gpus)
     out = run_rank(args)

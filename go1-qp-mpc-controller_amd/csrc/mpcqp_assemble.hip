@@ -100,4 +100,26 @@ hipError_t launch_assemble(int horizon, const double* states, int batch, double*
   return as::dispatch(horizon, states, batch, recs, stream, std::make_integer_sequence<int, MPCQP_MAX_HORIZON>{});
 }
 
+namespace as {
+// Indexed slot copy: dst[dst_idx[i]] = src[src_idx[i]] (identity where an index array is null), one
+// 256-thread block per slot, coalesced along the slot.
+__global__ void __launch_bounds__(256) copy_slots_kernel(const double* __restrict__ src, const int* __restrict__ sidx,
+                                                         double* __restrict__ dst, const int* __restrict__ didx,
+                                                         int count, int slot) {
+  const int i = blockIdx.x;
+  if (i >= count) return;
+  const double* s = src + (size_t)slot * (sidx ? sidx[i] : i);
+  double* d = dst + (size_t)slot * (didx ? didx[i] : i);
+  for (int e = threadIdx.x; e < slot; e += 256) d[e] = s[e];
+}
+}  // namespace as
+
+hipError_t launch_copy_slots(const double* src, const int* sidx, double* dst, const int* didx, int count, int slot,
+                             void* stream) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(as::copy_slots_kernel, dim3((unsigned)count), dim3(256), 0, (hipStream_t)stream, src, sidx, dst,
+                     didx, count, slot);
+  return hipGetLastError();
+}
+
 }  // namespace mpcqp

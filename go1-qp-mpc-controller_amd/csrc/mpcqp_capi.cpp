@@ -398,6 +398,17 @@ int32_t mpcqp_assemble_records_device(int32_t horizon, const double* d_states, i
   return mpcqp::launch_assemble(horizon, d_states, batch, d_records, stream) == hipSuccess ? MPCQP_OK : MPCQP_ERR_HIP;
 }
 
+int32_t mpcqp_copy_warm_slots_device(int32_t horizon, const double* d_src, const int32_t* d_src_idx, double* d_dst,
+                                     const int32_t* d_dst_idx, int32_t count, void* stream) {
+  if (horizon < 1 || horizon > MPCQP_MAX_HORIZON || count < 0 || (count > 0 && (!d_src || !d_dst)))
+    return MPCQP_ERR_INVALID_ARG;
+  if (count == 0) return MPCQP_OK;
+  return mpcqp::launch_copy_slots(d_src, d_src_idx, d_dst, d_dst_idx, count, mpcqp_warm_state_size(horizon), stream) ==
+                 hipSuccess
+             ? MPCQP_OK
+             : MPCQP_ERR_HIP;
+}
+
 void mpcqp_balance_default_params(mpcqp_balance_params* p) {
   if (!p) return;
   const double q[6] = {1.0, 1.0, 1.0, 400.0, 400.0, 100.0};  // A1RobotControl.cpp:11

@@ -63,6 +63,9 @@ hipError_t launch_torques(const double* recs, const mpcqp_result* grf, int batch
 
 // Input assembly from raw robot state (mpcqp_assemble.hip)
 hipError_t launch_assemble(int horizon, const double* states, int batch, double* recs, void* stream);
+// Indexed copy of fixed-size slots (warm-start slots of mixed-mode batches; mpcqp_assemble.hip)
+hipError_t launch_copy_slots(const double* src, const int* sidx, double* dst, const int* didx, int count, int slot,
+                             void* stream);
 
 // Single-step QP balance controller (mpcqp_balance.hip)
 hipError_t launch_balance(const mpcqp_balance_params& bp, const mpcqp_params& p, const double* recs, int batch,

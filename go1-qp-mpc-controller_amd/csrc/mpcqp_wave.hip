@@ -63,6 +63,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   using WL = WarmLayout<N>;
   using SI = ScaleImg<N>;
   constexpr int n = C::n, m = C::m, NTS = SC::NTS;
+  static_assert(NTS >= 64 + N, "wave 1 screens one horizon step per lane");
   __shared__ ScaleSmem<N> sm;
   const int inst = blockIdx.x;
   if (inst >= batch) return;
@@ -623,7 +624,7 @@ template <int N, int KS>
 __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, const double* __restrict__ recs,
                                            mpcqp_result* __restrict__ results, double* __restrict__ solution,
                                            double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
-                                           const double* __restrict__ img, const mpcqp_params& p,
+                                           double* __restrict__ img, const mpcqp_params& p,
                                            int* __restrict__ fb) {
   using C = Cfg<N>;
   using WL = WarmLayout<N>;
@@ -705,7 +706,8 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
 
   // ---- 3. OSQP scale_data: the image scale_kernel wrote (D, E, q~, c, branch; raw q if warm) ------
   using SI = ScaleImg<N>;
-  const double* im = img + (size_t)inst * SI::SIZE;
+  // (not const: the Schur form records max S_ii of its latest factorization in the DEGEN slot)
+  double* const im = img + (size_t)inst * SI::SIZE;
   const double c_s = im[SI::CS];
   const int mode = (int)im[SI::MODE];  // 0 cold, 1 osqp_update_P, 2 OsqpEigen re-init
   if (KS == 1 && im[SI::DEGEN] != 0.0) {
@@ -1013,7 +1015,7 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
         // allocation) and is handed to the Riccati form (wave_fallback_kernel), which solves it
         // from the start; nothing of it has been written.  max S_ii of the latest factorization
         // lives in the robot's image slot, not in a loop-carried register.
-        if (t == 0) const_cast<double*>(im)[SI::DEGEN] = smax;
+        if (t == 0) im[SI::DEGEN] = smax;
       }
       wave_sync();
 #ifdef MPCQP_REPEAT_FACTOR
@@ -1661,7 +1663,7 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                                                      mpcqp_result* __restrict__ results,
                                                      double* __restrict__ solution, double* __restrict__ trace,
                                                      int trace_cap, double* __restrict__ wstate,
-                                                     const double* __restrict__ img, mpcqp_params p,
+                                                     double* __restrict__ img, mpcqp_params p,
                                                      int* __restrict__ fb) {
   __shared__ WSmem<N, KS> sm;
   const int inst = blockIdx.x;
@@ -1677,7 +1679,7 @@ __global__ __launch_bounds__(NT, 1) void wave_fallback_kernel(const double* __re
                                                               double* __restrict__ solution,
                                                               double* __restrict__ trace, int trace_cap,
                                                               double* __restrict__ wstate,
-                                                              const double* __restrict__ img, mpcqp_params p,
+                                                              double* __restrict__ img, mpcqp_params p,
                                                               const int* __restrict__ fb) {
   __shared__ WSmem<N, 0> sm;
   const int cnt = fb[0];

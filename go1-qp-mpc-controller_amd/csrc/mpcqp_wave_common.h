@@ -631,7 +631,9 @@ struct ScaleCfg {
 #endif
   static constexpr int TPC = HREG ? MPCQP_SCALE_TPC : MPCQP_SCALE_TPC_LONG;  // threads per column (adjacent lanes)
   static constexpr int BPT = (N + TPC - 1) / TPC;    // horizon blocks of the column per thread
-  static constexpr int NTS = ((TPC * n + 63) / 64) * 64;
+  // at least two waves: wave 1 runs the degenerate-feet screen (one lane per horizon step) while
+  // wave 0 runs the gradient sweep, so N <= 5 (n <= 60) still launches threads 64 .. 64 + N - 1
+  static constexpr int NTS = ((TPC * n + 63) / 64) * 64 > 64 + N ? ((TPC * n + 63) / 64) * 64 : ((64 + N + 63) / 64) * 64;
   static constexpr int NWS = NTS / 64;
   // waves per SIMD the register allocation must allow (launch bounds): N = 10, two waves per robot,
   // four robots per CU; N = 20, four waves per robot, three per CU (measured, profiles/r04/occ)

@@ -105,7 +105,7 @@ EXPORTED = [
     "mpcqp_warm_state_size", "mpcqp_solve_batch_warm_device",
     "mpcqp_balance_default_params", "mpcqp_balance_solve_device", "mpcqp_assemble_records_device",
     "mpcqp_balance_solve_host", "mpcqp_solve_batch_warm_host",
-    "mpcqp_debug_scale_image_doubles", "mpcqp_debug_scale_image_device",
+    "mpcqp_debug_scale_image_doubles", "mpcqp_debug_scale_image_device", "mpcqp_copy_warm_slots_device",
 ]
 
 _libs = {}
@@ -179,6 +179,8 @@ def load(debug=False):
     L.mpcqp_balance_solve_host.restype = i32
     L.mpcqp_assemble_records_device.argtypes = [i32, vp, i32, vp, vp]
     L.mpcqp_assemble_records_device.restype = i32
+    L.mpcqp_copy_warm_slots_device.argtypes = [i32, vp, vp, vp, vp, i32, vp]
+    L.mpcqp_copy_warm_slots_device.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):
@@ -206,6 +208,13 @@ def assemble_records_device(horizon, d_states, batch, d_records, stream=0):
     """mpcqp_assemble_records_device: raw-state rows [batch][ST_SIZE] -> MPC records, on the device."""
     check(load().mpcqp_assemble_records_device(int(horizon), d_states, int(batch), d_records, stream or None),
           None, "mpcqp_assemble_records_device")
+
+
+def copy_warm_slots_device(horizon, d_src, d_src_idx, d_dst, d_dst_idx, count, stream=None):
+    """mpcqp_copy_warm_slots_device: slot d_dst[dst_idx[i]] = slot d_src[src_idx[i]] (device int32
+    index arrays, None = identity), i < count."""
+    check(load().mpcqp_copy_warm_slots_device(int(horizon), d_src, d_src_idx or None, d_dst, d_dst_idx or None,
+                                                int(count), stream or None), None, "mpcqp_copy_warm_slots_device")
 
 
 def default_balance_params(**over):

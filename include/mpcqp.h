@@ -156,6 +156,16 @@ int32_t mpcqp_warm_state_size(int32_t horizon);
 int32_t mpcqp_solve_batch_warm_device(mpcqp_handle* h, const double* d_records, int32_t batch, double* d_state,
                                       mpcqp_result* d_results, double* d_solution, void* stream);
 
+/* Indexed copy of warm-start slots between DEVICE buffers, for callers whose solved robots are a
+ * subset of their slots (a mixed-mode batch: the MPC robots' slots gathered into a compact buffer
+ * for the warm solve and scattered back after it, as the reference's controller keeps its member
+ * solver untouched on QP ticks, A1RobotControl.cpp:377-444).  For i < count:
+ *   slot d_dst[d_dst_idx ? d_dst_idx[i] : i] = slot d_src[d_src_idx ? d_src_idx[i] : i],
+ * slots of mpcqp_warm_state_size(horizon) doubles, index arrays DEVICE int32 (NULL = identity).
+ * Destination slots must be distinct.  Async on `stream`. */
+int32_t mpcqp_copy_warm_slots_device(int32_t horizon, const double* d_src, const int32_t* d_src_idx, double* d_dst,
+                                     const int32_t* d_dst_idx, int32_t count, void* stream);
+
 /* Host-pointer convenience wrapper (copies in, solves, copies out, synchronizes) on a stream of the
  * handle's own.  That stream is a blocking stream: it waits for work queued before the call on the
  * legacy NULL stream (zeroing warm slots with hipMemset(..) / on torch's default stream is ordered

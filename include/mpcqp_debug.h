@@ -42,6 +42,9 @@ int32_t mpcqp_debug_set_solver(mpcqp_handle* h, int32_t path);
  *   scaled gradient re-scaled), [44N, 56N) this tick's raw gradient q (warm slots), [56N] c,
  *   [56N + 1] branch (0 cold, 1 osqp_update_P, 2 OsqpEigen re-init), [56N + 2] 1 if some step's
  *   B6_k is rank deficient (collinear / coincident feet: the robot is solved by the Riccati form).
+ *   (During a solve the Schur-form wave kernel reuses slot 56N + 2, after reading the flag, for
+ *   max S_ii of its latest factorization: 1.0, or 2 SCHUR_SMAX when that exceeded SCHUR_SMAX and the
+ *   robot is handed to the Riccati form.  This entry point runs scale_kernel alone.)
  * d_state: warm slots as for mpcqp_solve_batch_warm_device, or NULL (cold).  Note that the pass
  * records H's zero pattern into the slots (as the solve's own pass does): run it on a copy.
  * libmpcqp_debug.so only (the product library returns MPCQP_ERR_INVALID_ARG). */

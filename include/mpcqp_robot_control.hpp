@@ -585,6 +585,16 @@ int control_type_of(const S& s) {
   else return 1;
 }
 
+// state types carrying the terrain-adaptation fields (A1CtrlStates.h:332, :370; Go1CtrlStates.hpp:337,
+// :375): use_terrain_adapt, terrain_pitch_angle, foot_pos_recent_contact (3x4)
+template <class S, class = void>
+struct has_terrain_fields : std::false_type {};
+template <class S>
+struct has_terrain_fields<S, std::void_t<decltype(std::declval<const S&>().use_terrain_adapt),
+                                         decltype(std::declval<S&>().terrain_pitch_angle = 0.0),
+                                         decltype(std::declval<const S&>().foot_pos_recent_contact(2, 0) + 0.0)>>
+    : std::true_type {};
+
 template <class InertiaOf, int N = 10>
 class RobotControlT {
  public:
@@ -600,6 +610,7 @@ class RobotControlT {
       DeviceScope ds(device_);
       (void)hipFree(d_state_);
       (void)hipFree(d_gather_);
+      (void)hipFree(d_idx_);
     }
     if (h_) mpcqp_destroy(h_);
   }
@@ -614,6 +625,22 @@ class RobotControlT {
   // call is a fresh cold solve (test_mpc.cpp:131-133).
   bool warm_start = true;
   double mu = 0.3, fz_min = 0.0, fz_max = 180.0;
+
+  // Terrain adaptation (A1RobotControl.cpp:334-376), on MPC ticks only (:335).  When this hook is
+  // set, compute_grf / compute_grf_batch apply the reference's state mutation to each MPC robot b
+  // before its record is assembled, so x_ref carries the adapted pitch (:475-476):
+  //   terrain_angle = root_pos[2] > 0.1 ? terrain_angle_of(b) : 0, clamped to [-0.5, 0.5];
+  //   F_R_diff = z(FL) + z(FR) - z(RL) - z(RR) of foot_pos_recent_contact;
+  //   if use_terrain_adapt: root_euler_d[1] = F_R_diff > 0.05 ? -terrain_angle : terrain_angle;
+  //   terrain_pitch_angle = terrain_angle.
+  // The hook returns the reference's filtered dihedral angle,
+  //   terrain_angle_filter.CalculateAverage(Utils::cal_dihedral_angle(flat_ground_coef,
+  //                                                                 compute_walking_surface(state)))
+  // and is called exactly where the reference updates that filter (only when root_pos[2] > 0.1), so
+  // the caller's filter sees the same sequence of samples; the plane fit and the filter stay with the
+  // caller.  Unset: no terrain adaptation (pass an adapted root_euler_d yourself).  The
+  // state type must carry use_terrain_adapt, terrain_pitch_angle and foot_pos_recent_contact.
+  std::function<double(int)> terrain_angle_of;
 
   // A1RobotControl.cpp:452-514: mutates state.mpc_states / mpc_states_d / root_lin_vel_d_world
   // exactly like the reference, and writes the record for the solve.
@@ -698,6 +725,8 @@ class RobotControlT {
       const int nm = (int)mpc_idx_.size();
       recs_.resize((size_t)nm * MPCQP_REC_SIZE(N));
       sub_res_.resize(nm);
+      if (terrain_angle_of)
+        for (int i = 0; i < nm; ++i) adapt_terrain(states[mpc_idx_[i]], mpc_idx_[i]);
       for (int i = 0; i < nm; ++i) assemble(states[mpc_idx_[i]], &recs_[(size_t)i * MPCQP_REC_SIZE(N)], hdt);
       if (warm_start) {
         ensure_slots(count);
@@ -705,17 +734,21 @@ class RobotControlT {
           throw_on(mpcqp_solve_batch_warm_host(h_, recs_.data(), nm, d_state_, sub_res_.data(), nullptr), h_,
                    "mpcqp_solve_batch_warm_host");
         } else {  // the MPC robots' slots, gathered and scattered back around the solve
+          // (one indexed-copy kernel each way on the legacy NULL stream, which the handle's
+          // blocking stream waits for; the index list is uploaded only when it changes)
           DeviceScope ds(device_);
-          const size_t sd = slot_doubles();
           ensure_gather(nm);
-          for (int i = 0; i < nm; ++i)
-            hip_ok(hipMemcpy(d_gather_ + sd * i, d_state_ + sd * mpc_idx_[i], sizeof(double) * sd,
-                             hipMemcpyDeviceToDevice), "hipMemcpy");
+          if (mpc_idx_ != dev_idx_) {
+            hip_ok(hipMemcpy(d_idx_, mpc_idx_.data(), sizeof(int) * nm, hipMemcpyHostToDevice), "hipMemcpy");
+            dev_idx_ = mpc_idx_;
+          }
+          throw_on(mpcqp_copy_warm_slots_device(N, d_state_, d_idx_, d_gather_, nullptr, nm, nullptr), nullptr,
+                   "mpcqp_copy_warm_slots_device");
           throw_on(mpcqp_solve_batch_warm_host(h_, recs_.data(), nm, d_gather_, sub_res_.data(), nullptr), h_,
                    "mpcqp_solve_batch_warm_host");
-          for (int i = 0; i < nm; ++i)
-            hip_ok(hipMemcpy(d_state_ + sd * mpc_idx_[i], d_gather_ + sd * i, sizeof(double) * sd,
-                             hipMemcpyDeviceToDevice), "hipMemcpy");
+          throw_on(mpcqp_copy_warm_slots_device(N, d_gather_, nullptr, d_state_, d_idx_, nm, nullptr), nullptr,
+                   "mpcqp_copy_warm_slots_device");
+          hip_ok(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
         }
       } else {
         throw_on(mpcqp_solve_batch_host(h_, recs_.data(), nm, sub_res_.data(), nullptr), h_, "mpcqp_solve_batch_host");
@@ -745,7 +778,7 @@ class RobotControlT {
   // :377-444; 1: MPC warm-started from this controller's previous MPC call, :446-562).  Like the
   // reference, the MPC horizon step is mpc_dt = 0.0025 and `dt` only with use_sim_time (:458-467).
   // A leg whose MPC solution norm is NaN keeps a zero column (the reference leaves it uninitialised).
-  // Terrain adaptation (:335-376) is upstream: pass the adapted root_euler_d.
+  // Terrain adaptation (:335-376): set terrain_angle_of (above), or pass an adapted root_euler_d.
   template <class State>
   Matrix34 compute_grf(State& state, double dt) {
     double f[12];
@@ -834,6 +867,27 @@ class RobotControlT {
       for (int l = 0; l < 4; ++l) foot_forces_grf(r, l) = f[r * 4 + l];
   }
 
+  // The state mutation of A1RobotControl.cpp:340-375 for MPC robot b (terrain_angle_of set).
+  template <class State>
+  void adapt_terrain(State& s, int b) const {
+    if constexpr (has_terrain_fields<State>::value) {
+      double terrain_angle = 0;
+      if (s.root_pos[2] > 0.1) terrain_angle = terrain_angle_of(b);  // the filter samples only here
+      if (terrain_angle > 0.5) terrain_angle = 0.5;
+      if (terrain_angle < -0.5) terrain_angle = -0.5;
+      const double f_r_diff = s.foot_pos_recent_contact(2, 0) + s.foot_pos_recent_contact(2, 1) -
+                              s.foot_pos_recent_contact(2, 2) - s.foot_pos_recent_contact(2, 3);
+      if (s.use_terrain_adapt) s.root_euler_d[1] = f_r_diff > 0.05 ? -terrain_angle : terrain_angle;
+      s.terrain_pitch_angle = terrain_angle;
+    } else {
+      (void)s;
+      (void)b;
+      throw std::invalid_argument(
+          "compute_grf: terrain_angle_of is set but the state type has no use_terrain_adapt / "
+          "terrain_pitch_angle / foot_pos_recent_contact");
+    }
+  }
+
   mpcqp_handle* handle() const { return h_; }
   int device() const { return device_; }
   const double* warm_slots() const { return d_state_; }
@@ -854,9 +908,13 @@ class RobotControlT {
     if (count <= gather_cap_ && d_gather_) return;
     DeviceScope ds(device_);
     if (d_gather_) hip_ok(hipFree(d_gather_), "hipFree");
+    if (d_idx_) hip_ok(hipFree(d_idx_), "hipFree");
     d_gather_ = nullptr;
+    d_idx_ = nullptr;
+    dev_idx_.clear();
     gather_cap_ = 0;
     hip_ok(hipMalloc(&d_gather_, sizeof(double) * slot_doubles() * count), "hipMalloc");
+    hip_ok(hipMalloc(&d_idx_, sizeof(int) * count), "hipMalloc");
     gather_cap_ = count;
   }
 
@@ -867,6 +925,8 @@ class RobotControlT {
   int slots_ = 0;
   double* d_gather_ = nullptr;  // mixed-mode batches: the MPC robots' slots, compacted
   int gather_cap_ = 0;
+  int* d_idx_ = nullptr;         // device copy of mpc_idx_ (gather / scatter index list)
+  std::vector<int> dev_idx_;     // what d_idx_ holds
   std::vector<int> mpc_idx_, qp_idx_;
   std::vector<mpcqp_result> sub_res_;
   std::vector<double> recs_;

@@ -47,3 +47,20 @@ def rel_err_u0(a, b):
     a = np.asarray(a).reshape(-1, 12)
     b = np.asarray(b).reshape(-1, 12)
     return np.max(np.abs(a - b), axis=1) / np.maximum(np.max(np.abs(b), axis=1), 1.0)
+
+
+def sentinel(err, bound, label):
+    """Regression sentinel at the accuracy the engine achieves (the SURVEY §8(c) 1e-4 gate stays in
+    each test as well): prints the measured maximum, appends it to $MPCQP_SENTINEL_LOG (JSON lines)
+    when set, and fails above `bound` unless $MPCQP_SENTINEL_CALIBRATE is set."""
+    import json
+    import os
+    m = float(np.max(err)) if np.size(err) else 0.0
+    print(f"[sentinel] {label}: max u0 rel err {m:.3e} (sentinel {bound:.0e})")
+    log = os.environ.get("MPCQP_SENTINEL_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(json.dumps({"label": label, "max_rel_err_u0": m, "sentinel": bound}) + "\n")
+    if not os.environ.get("MPCQP_SENTINEL_CALIBRATE"):
+        assert m <= bound, f"{label}: u0 error {m:.3e} above the regression sentinel {bound:.0e}"
+    return m

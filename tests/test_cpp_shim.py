@@ -237,3 +237,85 @@ def test_cpp_compute_grf_dispatches_on_stance_leg_control_type(oracle, tmp_path)
                     fb = np.array(r["f_body"]).reshape(4, 3).T
                     assert np.max(np.abs(grf[(t, b)] - fb)) <= 1e-4 * max(np.max(np.abs(fb)), 1.0)
     assert n_qp > 0 and n_mpc > 0
+
+
+@pytest.mark.gpu
+def test_cpp_terrain_adaptation_behind_compute_grf(oracle, tmp_path):
+    """Terrain adaptation behind the same compute_grf call (A1RobotControl.cpp:334-376): with the
+    shim's terrain_angle_of hook set, MPC ticks clamp the filtered angle to +-0.5 (0 when
+    root_pos[2] <= 0.1, where the hook is not called), set root_euler_d[1] by the front/rear
+    recent-contact height difference and terrain_pitch_angle; the adapted pitch reaches x_ref, so
+    u0 matches the oracle's persistent solver on records assembled from the adapted states."""
+    exe = os.path.join(REPO, "tests", "cpp", "build", "test_mode_switch_gpu")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(REPO, "tests", "cpp")], check=True)
+    T, B = 14, 4
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=47, gait="trot", swing_ticks=5)
+    for t in (2, 3, 9):  # a low body: no terrain sample (:341-345)
+        ticks[t].root_pos[1, 2] = 0.08
+    rows = np.stack([mpcqp.pack_states(st) for st in ticks])
+    path = tmp_path / "states.bin"
+    np.ascontiguousarray(rows, dtype=np.float64).tofile(path)
+    out = subprocess.run([exe, str(path), str(T), str(B), "terrain"], check=True, capture_output=True, text=True,
+                         timeout=120).stdout
+    got = {"TICK": {}, "BATCH": {}}
+    terr = {"TICK": {}, "BATCH": {}}
+    calls = {}
+    for line in out.splitlines():
+        p = line.split()
+        if p[0] in got:
+            # TICK / BATCH t b type status iters rho_updates u0[12]
+            got[p[0]][(int(p[1]), int(p[2]))] = (int(p[4]), int(p[5]), int(p[6]), np.array([float(x) for x in p[7:]]))
+        elif p[0] == "TERRAIN":
+            terr[p[1]][(int(p[2]), int(p[3]))] = (float(p[4]), float(p[5]))
+        elif p[0] == "HOOKCALLS":
+            calls[p[1]] = int(p[2])
+
+    def mode(t, b):
+        return 0 if (t + b) % 8 in (3, 4) else 1
+
+    def recent_z(t, b, l):
+        return -0.3 + 0.04 * ((3 * t + b + l) % 4)
+    expect_calls = 0
+    n_neg = n_clamped = 0
+    for t in range(T):
+        for b in range(B):
+            if mode(t, b) != 1:
+                assert (t, b) not in terr["TICK"]
+                continue
+            high = ticks[t].root_pos[b, 2] > 0.1
+            expect_calls += int(high)
+            ang = 0.7 * np.sin(0.9 * t + 1.7 * b) if high else 0.0
+            n_clamped += int(abs(ang) > 0.5)
+            ang = min(max(ang, -0.5), 0.5)
+            frd = recent_z(t, b, 0) + recent_z(t, b, 1) - recent_z(t, b, 2) - recent_z(t, b, 3)
+            e1 = -ang if frd > 0.05 else ang
+            n_neg += int(frd > 0.05 and ang != 0.0)
+            for tag in ("TICK", "BATCH"):
+                g1, gp = terr[tag][(t, b)]
+                assert abs(gp - ang) <= 1e-15 and abs(g1 - e1) <= 1e-15, (tag, t, b, g1, e1, gp, ang)
+            assert terr["TICK"][(t, b)] == terr["BATCH"][(t, b)]
+            ticks[t].root_euler_d[b, 1] = terr["TICK"][(t, b)][0]  # the adapted state, bit for bit
+    assert calls == {"TICK": expect_calls, "BATCH": expect_calls}
+    assert n_neg > 0 and n_clamped > 0 and expect_calls < sum(mode(t, b) for t in range(T) for b in range(B))
+    recs_t = np.stack([mpcqp.assemble_compute_grf(st, 10) for st in ticks])
+    op = oracle.default_params(10)
+    moved = 0.0
+    for b in range(B):
+        mts = [t for t in range(T) if mode(t, b) == 1]
+        ref_m = oracle.solve_sequence(op, np.ascontiguousarray(recs_t[mts, b:b + 1]), nthreads=1)
+        for i, t in enumerate(mts):
+            r = ref_m[i][0]
+            for tag in ("TICK", "BATCH"):
+                st, it, ru, u0 = got[tag][(t, b)]
+                assert (st, it) == (int(r["status"]), int(r["iters"])), (tag, t, b)
+                err = np.max(np.abs(u0 - r["u0"])) / max(np.max(np.abs(r["u0"])), 1.0)
+                assert err <= 1e-4, (tag, t, b, err)
+            # x_ref's pitch row is the adapted one
+            xr = recs_t[t, b, mpcqp._lib.REC_XREF:mpcqp._lib.REC_XREF + 130].reshape(10, 13)
+            assert np.all(xr[:, 1] == terr["TICK"][(t, b)][0])
+        plain = [mpcqp.assemble_compute_grf(st, 10)[b] for st in mpcqp.records.synthetic_go1_ticks(
+            B, T, seed=47, gait="trot", swing_ticks=5)]
+        ref_p = oracle.solve_sequence(op, np.ascontiguousarray(np.stack([plain[t] for t in mts])[:, None]), nthreads=1)
+        moved = max(moved, max(np.max(np.abs(ref_p[i][0]["u0"] - got["TICK"][(t, b)][3])) for i, t in enumerate(mts)))
+    assert moved > 1e-3  # the adaptation changes the forces, so the comparison above can see it

@@ -62,7 +62,7 @@ def test_shard_range_partitions():
             assert max(sizes) - min(sizes) <= 1
 
 
-@pytest.mark.parametrize("world,batch", [(2, 48), (3, 16), (8, None)])
+@pytest.mark.parametrize("world,batch", [(1, 32), (2, 48), (3, 16), (8, None)])
 def test_bench_launcher_shards_and_gathers(world, batch):
     """bench.py --gpus N as the driver runs it: the parent starts torch.distributed.run as a child
     (no GPU touched), N ranks take contiguous shards of ONE seeded global batch, run the production
@@ -74,6 +74,8 @@ def test_bench_launcher_shards_and_gathers(world, batch):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     argv = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(world), "--cpu-stub",
             "--steps", "2", "--warmup", "1"]
+    if world == 1:  # the distributed branch at world 1 (what tests/test_gpu_rccl.py runs over RCCL)
+        argv.append("--dist")
     if batch is not None:
         argv += ["--batch", str(batch)]
     else:  # the driver's 8-GPU line: no --batch, so the default must be C3 (8192 robots per GPU)

@@ -15,11 +15,11 @@ from gpu_helpers import rel_err_u0, solve_gpu
 pytestmark = pytest.mark.gpu
 
 N = 10
-F = mpcqp._lib.rec_feet(N)
 
 
-def _degenerate(recs):
+def _degenerate(recs, N=N):
     """Four kinds of rank-deficient feet, cycling over the given records."""
+    F = mpcqp._lib.rec_feet(N)
     out = recs.copy()
     line_x = np.array([[0.17, 0.0, -0.3], [0.05, 0.0, -0.3], [-0.05, 0.0, -0.3], [-0.17, 0.0, -0.3]])
     diag = np.array([[0.17, 0.15, -0.3], [0.06, 0.053, -0.3], [-0.06, -0.053, -0.3], [-0.17, -0.15, -0.3]])
@@ -39,9 +39,11 @@ def _degenerate(recs):
 
 
 @pytest.mark.parametrize("gait", ["trot", "stance", "mixed"])
-def test_degenerate_feet_match_oracle(oracle, gait):
+@pytest.mark.parametrize("N", [1, 3, 5, 10])
+def test_degenerate_feet_match_oracle(oracle, gait, N):
+    """Every Schur horizon (at N <= 5 the screen's wave did not exist)."""
     st = mpcqp.synthetic_go1(32, seed=911, gait=gait, mixed_mu=(gait == "mixed"))
-    recs = _degenerate(mpcqp.assemble_compute_grf(st, N))
+    recs = _degenerate(mpcqp.assemble_compute_grf(st, N), N)
     with mpcqp.MpcQpSolver(mpcqp.default_params(N)) as s:
         got, sol, _ = solve_gpu(s, recs)
     ref = oracle.solve_batch(oracle.default_params(N), recs, nthreads=8)
@@ -51,11 +53,13 @@ def test_degenerate_feet_match_oracle(oracle, gait):
     assert np.all(rel_err_u0(got["u0"], ref["u0"]) <= 1e-4)
 
 
-def test_degenerate_flag_in_scale_image(oracle):
-    """The screen flags exactly the rank-deficient robots (debug library image, slot 56N + 2)."""
+@pytest.mark.parametrize("N", [1, 2, 5, 6, 10])
+def test_degenerate_flag_in_scale_image(oracle, N):
+    """The screen flags exactly the rank-deficient robots (debug library image, slot 56N + 2) at
+    every Schur horizon, the one-wave scale launches (N <= 5) included."""
     st = mpcqp.synthetic_go1(16, seed=912, gait="trot")
     recs = mpcqp.assemble_compute_grf(st, N)
-    recs[::2] = _degenerate(recs[::2])
+    recs[::2] = _degenerate(recs[::2], N)
     with mpcqp.MpcQpSolver(mpcqp.default_params(N), debug=True) as s:
         d_rec = torch.from_numpy(recs).cuda()
         d_img = torch.zeros((16, s.scale_image_size), dtype=torch.float64, device="cuda")

@@ -1,0 +1,44 @@
+"""C3's collective path on a real MI355X at world size 1 (BASELINE.json configs[2]).
+
+bench.py --gpus 1 --dist starts `torch.distributed.run --nproc-per-node 1` as a CHILD process (the
+test process never execs), and the rank takes the same branch an 8-GPU rank takes:
+init_process_group("nccl", device_id=...) (RCCL on ROCm), the solve plus
+mpcqp.distributed.allgather_forces inside the timed loop, the all-gather's HIP-event span
+(extras.allgather_ms, max over ranks) and the gathered-u0 check, then oracle parity on the sample.
+This is no scaling measurement: one rank, one GPU."""
+import json
+import math
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_rccl_world1_gathers_and_matches_oracle():
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    argv = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--dist",
+            "--steps", "4", "--warmup", "1", "--batch", "2048"]
+    out = subprocess.run(argv, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-3000:]
+    rec = json.loads(lines[0])
+    print(json.dumps({k: rec[k] for k in ("value", "ms_per_step", "extras", "parity")}))
+    assert rec["n_gpus"] == 1 and rec["config"]["ranks_seen"] == 1
+    assert rec["config"]["collective"].startswith("RCCL")
+    ex = rec["extras"]
+    assert ex["backend"] == "nccl"
+    assert math.isfinite(ex["allgather_ms"]) and ex["allgather_ms"] >= 0.0
+    assert math.isfinite(ex["solve_kernel_ms_max_over_ranks"]) and ex["solve_kernel_ms_max_over_ranks"] > 0.0
+    par = rec["parity"]
+    assert par["gathered_u0_equals_rank_results"]
+    assert par["instances"] == 2048
+    assert par["status_equal"] and par["iters_equal"]
+    assert par["max_rel_err_u0"] <= 1e-4
+    assert par["max_rel_err_u0"] <= 1e-8  # regression sentinel at the achieved accuracy (~1e-10)
