@@ -3,10 +3,10 @@
 
 One step = one pass of the hot path over one batch of synthetic robot states resident in HBM:
 scale_kernel (OSQP scale_data on the condensed Hessian's closed-form columns) + wave_kernel
-(OSQP-0.6 ADMM with the KKT solve in the impulse-space Schur form at N <= 10, the Riccati form with
-its factorization on MFMA above; extraction) + the Riccati fallback launch for robots with
-rank-deficient feet (an empty list at C2), and for N > 1 ranks the RCCL all-gather of the solved
-forces over xGMI (north_star, config C3).
+(OSQP-0.6 ADMM with the KKT solve in the impulse-space Schur form at N <= 10 -- the Riccati form, in
+the same wave, for robots with rank-deficient feet or an ill-conditioned Schur core (none at C2) --
+and the Riccati form with its factorization on MFMA above; extraction), and for N > 1 ranks the RCCL
+all-gather of the solved forces over xGMI (north_star, config C3).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--horizon 10]
 
@@ -344,7 +344,8 @@ def run_rank(args):
             out["cpu_baseline"] = out.get("cpu_baseline")
             out["stats"] = {"mean_iters": float(res_all["iters"].mean()), "max_iters": int(res_all["iters"].max()),
                             "mean_rho_updates": float(res_all["rho_updates"].mean()),
-                            "solved_frac": float(np.mean(res_all["status"] == 1))}
+                            "solved_frac": float(np.mean(res_all["status"] == 1)),
+                            "handoff_count": list(solver.handoff_counts()) if N <= 10 else None}
             if not dist_on and not args.no_extras:
                 out["extras"] = extras(args, solver, params, recs_np, states, local_res, pyoracle, dev)
     if solver is not None:
@@ -512,9 +513,13 @@ def extras(args, solver, params, recs_np, states, base_res, pyoracle, dev):
         r5 = torch.zeros((B5, RD), dtype=torch.float64, device=dev)
         ms = _timed(lambda: s5.solve_device(d5.data_ptr(), B5, r5.data_ptr(), 0, sp), steps, stream)
         g5 = res_of(r5)
+        h5 = s5.handoff_counts()
     ent = {"value": B5 / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms, "batch": B5, "horizon": 10,
            "workload": "C5: mixed gait, contacts ~ Bernoulli(0.5)^4, mu ~ U(0.3,0.9)",
-           "mean_iters": float(g5["iters"].mean())}
+           "mean_iters": float(g5["iters"].mean()),
+           "handoff_count": {"rank_deficient_feet": h5[0], "ill_conditioned_at_initial_rho": h5[1],
+                             "crossed_after_rho_update": h5[2],
+                             "what": "robots the Riccati form solved in their own wave (mpcqp_handoff_counts)"}}
     if pyoracle is not None:
         idx = np.unique(np.linspace(0, B5 - 1, 512).astype(np.int64))
         ref = pyoracle.solve_batch(pyoracle.default_params(10), rec5[idx], nthreads=nthr)

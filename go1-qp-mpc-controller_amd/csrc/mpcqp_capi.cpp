@@ -22,7 +22,7 @@ struct mpcqp_handle {
   double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
   size_t work_per = 0;       // doubles per instance the workspace was sized for
-  int* fb = nullptr;         // wave path: Schur -> Riccati fallback list [work_cap + 1] ints
+  int* fb = nullptr;         // wave path: the Schur -> Riccati hand-off counters of the last solve [4] ints
   int path = 0;              // 0 auto (= 3), 3 Riccati wave; debug library only: 1 dense K^-1, 2 Riccati workgroup
   // host wrapper: device buffers, a private stream and two pinned staging chunks
   hipStream_t hstream = nullptr;
@@ -111,7 +111,7 @@ hipError_t ensure_workspace(mpcqp_handle* h, int32_t batch, void* stream) {
   h->work_cap = 0;
   h->work_per = 0;
   if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * per * cap);
-  if (e == hipSuccess) e = hipMalloc(&h->fb, sizeof(int) * (cap + 1));
+  if (e == hipSuccess) e = hipMalloc(&h->fb, sizeof(int) * 4);
   if (e == hipSuccess) {
     h->work_cap = cap;
     h->work_per = per;
@@ -505,6 +505,17 @@ int32_t mpcqp_abi_sizes(int32_t* params_size, int32_t* result_size) {
 }
 
 int32_t mpcqp_handle_slots(mpcqp_handle* h) { return h ? h->slots : 0; }
+
+int32_t mpcqp_handoff_counts(mpcqp_handle* h, int32_t counts[3]) {
+  if (!h || !counts) return MPCQP_ERR_INVALID_ARG;
+  counts[0] = counts[1] = counts[2] = 0;
+  if (!h->fb) return MPCQP_OK;  // no wave solve yet
+  DeviceGuard g(h->device);
+  hipError_t e = g.err;
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(counts, h->fb, sizeof(int32_t) * 3, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? MPCQP_OK : set_hip_error(h, e, "mpcqp_handoff_counts");
+}
 
 int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {
   if (!h || batch < 0) return MPCQP_ERR_INVALID_ARG;

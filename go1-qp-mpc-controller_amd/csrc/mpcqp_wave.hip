@@ -68,7 +68,9 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   const int inst = blockIdx.x;
   if (inst >= batch) return;
   const int t = threadIdx.x;
-  if (inst == 0 && t == 0) fb[0] = 0;  // wave_kernel's fallback list starts empty (stream order)
+  // wave_kernel's hand-off counters start at zero (stream order): [0] rank-deficient feet, [1] an
+  // ill-conditioned Schur core at the initial rho (the pre-screen below), [2] one that crossed later
+  if (inst == 0 && t < 3) fb[t] = 0;
   {
     const double* rg = recs + (size_t)inst * C::REC;
     int bad = 0;
@@ -91,6 +93,7 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   }
   const double dtm = (1.0 / mass) * dt;
   // B_d(k) rows 6-8 (calculate_B_mat_c, Utils.cpp:35-41), gradient adjoint (ConvexMpc.cpp:215-217)
+  bool any_degen;
   {
     int degen = 0;
     double Iwinv[9];
@@ -201,9 +204,8 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
         }
       }
     }
-    // (written at once: nothing of the screen stays live through the Ruiz passes)
-    const int any_degen = __syncthreads_or(degen);
-    if (t == 0) img[(size_t)inst * ScaleImg<N>::SIZE + ScaleImg<N>::DEGEN] = any_degen ? 1.0 : 0.0;
+    // (a block-uniform flag: nothing else of the screen stays live through the Ruiz passes)
+    any_degen = __syncthreads_or(degen) != 0;
   }
   // thread t: column j0 = t / 4, blocks jb .. jb+BPT-1 of it (the column's four threads are a quad)
   constexpr int BPT = SC::BPT;
@@ -571,9 +573,26 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     if (ws) out[SI::QN + j0] = sm.qn[j0];
   }
   for (int r = t; r < m; r += NTS) out[SI::E + r] = Ec[r];
+  // The Schur form's hand-off flag: 1 rank-deficient B6_k (the screen above), 2 an ill-conditioned
+  // Schur core at the initial rho (max S_ii of the first factorization above SCHUR_SMAX), 0 neither;
+  // wave_kernel<N, 1> solves flagged robots by the Riccati form from the start.
+  double flag = any_degen ? 1.0 : 0.0;
+  if constexpr (N <= 10) {
+    if (!any_degen) {  // (block-uniform)
+      __shared__ PrescreenScratch<N> ps;
+      const double rho0 = mode == 1 ? ws[WL::RHO] : dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
+      double cont[4];
+#pragma unroll
+      for (int l = 0; l < 4; ++l) cont[l] = rec[MPCQP_REC_CONTACTS + l] != 0.0 ? 1.0 : 0.0;
+      if (schur_prescreen<N>(sm, ps, sm.Ap[0], sm.Ap[1], Dc, Ec, c_s, rho0, p, A, dtm, cont, rec[MPCQP_REC_FZMIN],
+                             rec[MPCQP_REC_FZMAX]))
+        flag = 2.0;
+    }
+  }
   if (t == 0) {
     out[SI::CS] = c_s;
     out[SI::MODE] = (double)mode;
+    out[SI::DEGEN] = flag;
   }
   SC_MARK(6);
 }
@@ -616,12 +635,13 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
 
 // KS: the KKT solve.  0 = Riccati recursion (chains over the horizon, factors on MFMA; every N),
 // 1 = impulse-space Schur form (mpcqp_schur.h; N <= 10, nonnegative state weights).
-// The solve of robot `inst` by one wave (the kernels below: one robot per workgroup, or the
-// Riccati fallback's list of robots).  KS = 1 robots whose G_k is (nearly) singular append
-// themselves to fb (fb[0] = count, fb[1..]) and return without writing anything: the fallback
-// kernel solves them with KS = 0.
+// The solve of robot `inst` by one wave (wave_kernel: one robot per workgroup).  Returns true when a
+// KS = 1 solve hands the robot to the Riccati form without having written anything: scale_kernel
+// flagged it (rank-deficient B6_k, or an ill-conditioned Schur core at the initial rho), or a later
+// factorization's max S_ii crossed SCHUR_SMAX; wave_kernel then solves it with KS = 0 in the same
+// wave.  fb[0..2] count the three cases.
 template <int N, int KS>
-__device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, const double* __restrict__ recs,
+__device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, const double* __restrict__ recs,
                                            mpcqp_result* __restrict__ results, double* __restrict__ solution,
                                            double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
                                            double* __restrict__ img, const mpcqp_params& p,
@@ -659,7 +679,7 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
       }
       if (solution)
         for (int e = t; e < n; e += NT) solution[(size_t)inst * n + e] = NAN;
-      return;
+      return false;
     }
   }
   wave_sync();
@@ -710,15 +730,15 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
   double* const im = img + (size_t)inst * SI::SIZE;
   const double c_s = im[SI::CS];
   const int mode = (int)im[SI::MODE];  // 0 cold, 1 osqp_update_P, 2 OsqpEigen re-init
-  if (KS == 1 && im[SI::DEGEN] != 0.0) {
-    // rank-deficient B6_k (collinear / coincident feet, scale_kernel's screen): G_k would be
-    // singular.  The reference QP is still strictly convex (R > 0); the Riccati form (KS = 0,
-    // wave_fallback_kernel) solves this robot.  Nothing of it has been written yet.
-    if (t == 0) {
-      const int j = atomicAdd(fb, 1);
-      fb[1 + j] = inst;
+  if (KS == 1) {
+    const double flag = im[SI::DEGEN];
+    if (flag != 0.0) {
+      // rank-deficient B6_k (collinear / coincident feet: G_k would be singular; the reference QP is
+      // still strictly convex, R > 0) or an ill-conditioned Schur core at the initial rho: the
+      // Riccati form (KS = 0) solves this robot.  Nothing of it has been written yet.
+      if (t == 0) atomicAdd(fb + (flag == 1.0 ? 0 : 1), 1);
+      return true;
     }
-    return;
   }
   for (int j = t; j < n; j += NT) {
     HS.D[j] = im[SI::D + j];
@@ -1012,8 +1032,8 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
         // (large state weights, four feet in contact) the difference loses digits the Riccati form
         // keeps.  Such a robot leaves the loop at the next need_info iteration (one follows every
         // factorization before the next one; an exit right here cost 8 % of the kernel in register
-        // allocation) and is handed to the Riccati form (wave_fallback_kernel), which solves it
-        // from the start; nothing of it has been written.  max S_ii of the latest factorization
+        // allocation) and is handed to the Riccati form (wave_kernel: the same wave), which solves
+        // it from the start; nothing of it has been written.  max S_ii of the latest factorization
         // lives in the robot's image slot, not in a loop-carried register.
         if (t == 0) im[SI::DEGEN] = smax;
       }
@@ -1569,11 +1589,8 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
 
   WV_MARK(20);
   if (KS == 1 && !(img_at(SI::DEGEN) <= SCHUR_SMAX)) {  // ill-conditioned S: the Riccati form solves it
-    if (t == 0) {
-      const int j = atomicAdd(fb, 1);
-      fb[1 + j] = inst;
-    }
-    return;
+    if (t == 0) atomicAdd(fb + 2, 1);
+    return true;
   }
   if (ws) {  // the solver persists: scaling, scaled data, iterates and rho for the next tick
     if (t == 0) {
@@ -1656,6 +1673,7 @@ __device__ __forceinline__ void wave_solve(const int inst, WSmem<N, KS>& sm, con
     res->iters = iters;
     res->rho_updates = rho_updates;
   }
+  return false;
 }
 
 template <int N, int KS>
@@ -1665,27 +1683,23 @@ __global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ 
                                                      int trace_cap, double* __restrict__ wstate,
                                                      double* __restrict__ img, mpcqp_params p,
                                                      int* __restrict__ fb) {
-  __shared__ WSmem<N, KS> sm;
   const int inst = blockIdx.x;
-  if (inst >= batch) return;
-  wave_solve<N, KS>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb);
-}
-
-// The robots wave_kernel<N, 1> handed over (fb[0] of them at fb[1..]), by the Riccati form; a
-// grid-stride loop over the list, so any grid size covers any count (0: every wave exits at once).
-template <int N>
-__global__ __launch_bounds__(NT, 1) void wave_fallback_kernel(const double* __restrict__ recs,
-                                                              mpcqp_result* __restrict__ results,
-                                                              double* __restrict__ solution,
-                                                              double* __restrict__ trace, int trace_cap,
-                                                              double* __restrict__ wstate,
-                                                              double* __restrict__ img, mpcqp_params p,
-                                                              const int* __restrict__ fb) {
-  __shared__ WSmem<N, 0> sm;
-  const int cnt = fb[0];
-  for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
-    wave_solve<N, 0>(fb[1 + j], sm, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr);
-    wave_sync();
+  if constexpr (KS == 1) {
+    // The Schur form, and in the same wave the Riccati form for the robots it hands over (the two
+    // forms' LDS images share one allocation: the Riccati factors fit inside the Schur core's)
+    __shared__ union LdsU {
+      WSmem<N, 1> s;
+      WSmem<N, 0> r;
+    } sm;
+    if (inst >= batch) return;
+    if (wave_solve<N, 1>(inst, sm.s, recs, results, solution, trace, trace_cap, wstate, img, p, fb)) {
+      wave_sync();
+      wave_solve<N, 0>(inst, sm.r, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr);
+    }
+  } else {
+    __shared__ WSmem<N, 0> sm;
+    if (inst >= batch) return;
+    wave_solve<N, 0>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb);
   }
 }
 
@@ -1727,12 +1741,6 @@ static hipError_t launch_wave(const LaunchArgs& a) {
     if (schur_ok(a.p)) {
       hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs,
                          a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
-      e = hipGetLastError();
-      if (e != hipSuccess) return e;
-      // the robots with (nearly) singular G_k, if any (an empty list costs one short launch)
-      const int grid = a.batch < FALLBACK_GRID ? a.batch : FALLBACK_GRID;
-      hipLaunchKernelGGL((wv::wave_fallback_kernel<N>), dim3(grid), dim3(wv::NT), 0, (hipStream_t)a.stream,
-                         a.recs, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
       return hipGetLastError();
     }
   }

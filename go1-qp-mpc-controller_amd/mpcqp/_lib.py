@@ -106,6 +106,7 @@ EXPORTED = [
     "mpcqp_balance_default_params", "mpcqp_balance_solve_device", "mpcqp_assemble_records_device",
     "mpcqp_balance_solve_host", "mpcqp_solve_batch_warm_host",
     "mpcqp_debug_scale_image_doubles", "mpcqp_debug_scale_image_device", "mpcqp_copy_warm_slots_device",
+    "mpcqp_handoff_counts",
 ]
 
 _libs = {}
@@ -181,6 +182,8 @@ def load(debug=False):
     L.mpcqp_assemble_records_device.restype = i32
     L.mpcqp_copy_warm_slots_device.argtypes = [i32, vp, vp, vp, vp, i32, vp]
     L.mpcqp_copy_warm_slots_device.restype = i32
+    L.mpcqp_handoff_counts.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
+    L.mpcqp_handoff_counts.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):

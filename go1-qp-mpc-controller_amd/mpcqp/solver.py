@@ -57,6 +57,15 @@ class MpcQpSolver:
     def reserve(self, batch):
         check(self._L.mpcqp_reserve(self._h, int(batch)), self._h, "mpcqp_reserve", self._L)
 
+    def handoff_counts(self):
+        """mpcqp_handoff_counts: robots of the last Schur-form solve that the Riccati form solved in
+        their own wave, as (rank-deficient feet, ill-conditioned at the initial rho, crossed later).
+        Synchronizes the device."""
+        import ctypes
+        c = (ctypes.c_int32 * 3)()
+        check(self._L.mpcqp_handoff_counts(self._h, c), self._h, "mpcqp_handoff_counts", self._L)
+        return tuple(int(v) for v in c)
+
     # -- device-pointer API ------------------------------------------------------------------------
     def solve_device(self, d_records, batch, d_results, d_solution=0, stream=0):
         """mpcqp_solve_batch_device: records/results/solution are device pointers (ints)."""

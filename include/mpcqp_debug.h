@@ -25,6 +25,12 @@ int32_t mpcqp_abi_sizes(int32_t* params_size, int32_t* result_size);
 /* Persistent-grid size (resident workgroups) chosen for the handle's device. */
 int32_t mpcqp_handle_slots(mpcqp_handle* h);
 
+/* Robots of the handle's last Schur-form (N <= 10) wave solve that the Riccati form solved in their
+ * own wave: counts[0] rank-deficient feet, counts[1] an ill-conditioned Schur core at the initial
+ * rho (scale_kernel's pre-screen, max S_ii > SCHUR_SMAX), counts[2] a core that crossed the
+ * threshold after a rho update (left the Schur form at a check).  Synchronizes the device. */
+int32_t mpcqp_handoff_counts(mpcqp_handle* h, int32_t counts[3]);
+
 /* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */
 int32_t mpcqp_solve_threads(int32_t horizon);
 

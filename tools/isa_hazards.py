@@ -228,8 +228,7 @@ def main():
                         f"-DMPCQP_WAVE_FOR_EACH_N(X)=X({a.n})", "--cuda-device-only", "-S", SRC, "-o", path] + a.defs,
                        check=True, stderr=subprocess.DEVNULL)
     text = open(path).read()
-    names = a.kernels or [f"wave_kernelILi{a.n}ELi1E", f"wave_kernelILi{a.n}ELi0E", f"scale_kernelILi{a.n}E"] + (
-        [f"wave_fallback_kernelILi{a.n}E"] if a.n <= 10 else [])
+    names = a.kernels or [f"wave_kernelILi{a.n}ELi1E", f"wave_kernelILi{a.n}ELi0E", f"scale_kernelILi{a.n}E"]
     total = 0
     for nm, lines, l0 in kernels(text, names):
         probs, nins = check(lines, l0)
