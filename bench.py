@@ -517,8 +517,7 @@ def extras(args, solver, params, recs_np, states, base_res, pyoracle, dev):
     ent = {"value": B5 / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms, "batch": B5, "horizon": 10,
            "workload": "C5: mixed gait, contacts ~ Bernoulli(0.5)^4, mu ~ U(0.3,0.9)",
            "mean_iters": float(g5["iters"].mean()),
-           "handoff_count": {"rank_deficient_feet": h5[0], "ill_conditioned_at_initial_rho": h5[1],
-                             "crossed_after_rho_update": h5[2],
+           "handoff_count": {"rank_deficient_feet": h5[0], "ill_conditioned_after_rho_update": h5[2],
                              "what": "robots the Riccati form solved in their own wave (mpcqp_handoff_counts)"}}
     if pyoracle is not None:
         idx = np.unique(np.linspace(0, B5 - 1, 512).astype(np.int64))

@@ -442,157 +442,6 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   wave_sync();
 }
 
-// ---- pre-screen (scale_kernel): max_i S_ii of the first factorization -----------------------------
-// Once scale_kernel's scaling is final it evaluates the S_ii that wave_kernel's first factorization
-// (at the initial rho) records, with schur_factor's expressions in the same order: R'_k foot blocks
-// from A~ = E A D and the rho vector (wave_solve's R' prologue), R'^-1 by cofactors, the rows of
-// B6 R'^-1, G_k, its Cholesky factor L_k, the lane's column of L and S_ii = 1 + beta_kk |v_i|^2 +
-// alpha_kk |w_i|^2.  A robot whose core is ill-conditioned from the start is then solved by the
-// Riccati form from its first iteration (wave_kernel, the same wave) instead of leaving the Schur form
-// at a check.  Every thread of the block calls it (two barriers); threads t < 4N write the R'^-1 foot
-// block of (step t / 4, leg t % 4), threads t < 6N (impulse unknown 6k + c) the B6 R'^-1 row c and G_k
-// row c; returns whether some S_ii exceeds SCHUR_SMAX (block-uniform).
-// ap0 / ap1: the unscaled constraint entries by row (on fx|fy / on fz, ConvexMpc.cpp:46-58), D / E
-// the final scaling, c_s the cost scale, rho0 the solve's initial rho, cont[4] the contact flags.
-template <int N>
-struct PrescreenScratch {
-  static constexpr int NI = 6 * N;
-  alignas(16) double Ri[N][4][9];
-  alignas(16) double B6R[NI][12];
-  alignas(16) double G[N][36];
-};
-template <int N, class SM>
-__device__ bool schur_prescreen(SM& sm, PrescreenScratch<N>& ps, const double* ap0, const double* ap1,
-                                const double* D, const double* E, double c_s, double rho0, const mpcqp_params& p,
-                                const Adisc& A, double dtm, const double (&cont)[4], double fzmin, double fzmax) {
-  constexpr int ND_ = 12, CD_ = 20, NI = 6 * N;
-  const int t = threadIdx.x;
-  const double sigma = p.sigma;
-  if (t < 4 * N) {  // R'_k foot block of (k, leg) (wave_solve's factorization prologue), then R'^-1
-    const int k = t >> 2, leg = t & 3;
-    const int cf = ND_ * k + 3 * leg;
-    double k0[4], k1[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int ri = CD_ * k + 5 * leg + a;
-      k0[a] = (ap0[ri] * E[ri]) * D[cf + (a >> 1)];
-      k1[a] = (ap1[ri] * E[ri]) * D[cf + 2];
-    }
-    const int r4 = CD_ * k + 5 * leg + 4;
-    const double ak4 = (ap1[r4] * E[r4]) * D[cf + 2];
-    double l4 = fzmin * cont[leg], u4 = fzmax * cont[leg];
-    l4 = dmin(dmax(l4, -OSQP_INF), OSQP_INF);
-    u4 = dmin(dmax(u4, -OSQP_INF), OSQP_INF);
-    const double L4 = E[r4] * l4, U4 = E[r4] * u4;
-    const bool loose = L4 < -OSQP_INF * MIN_SCALING && U4 > OSQP_INF * MIN_SCALING;
-    const bool eq = U4 - L4 < RHO_TOL;
-    const double rq4 = loose ? RHO_MIN : (eq ? RHO_EQ_OVER_RHO_INEQ * rho0 : rho0);
-    const double di[3] = {1. / D[cf], 1. / D[cf + 1], 1. / D[cf + 2]};
-    auto coef = [&](int row, int col) __attribute__((always_inline)) {
-      if (row == 4) return col == 2 ? ak4 : 0.0;
-      if (col == 2) return k1[row];
-      return (col == (row >> 1)) ? k0[row] : 0.0;
-    };
-    double m[3][3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        double s = 0.0;
-#pragma unroll
-        for (int row = 0; row < 5; ++row) s += (coef(row, a) * (row == 4 ? rq4 : rho0)) * coef(row, b);
-        m[a][b] = (a == b ? c_s * (2.0 * p.r_weights[3 * leg + a]) : 0.0) + (di[a] * ((a == b ? sigma : 0.0) + s)) * di[b];
-      }
-    // cofactor inverse of the symmetric block from its upper triangle (schur_factor)
-    const double m00 = m[0][0], m01 = m[0][1], m02 = m[0][2], m11 = m[1][1], m12 = m[1][2], m22 = m[2][2];
-    const double c00 = m11 * m22 - m12 * m12, c01 = m02 * m12 - m01 * m22, c02 = m01 * m12 - m02 * m11;
-    const double c11 = m00 * m22 - m02 * m02, c12 = m01 * m02 - m00 * m12, c22 = m00 * m11 - m01 * m01;
-    const double inv = recip((m00 * c00 + m01 * c01) + m02 * c02);
-    double* ri = ps.Ri[k][leg];
-    ri[0] = c00 * inv; ri[1] = c01 * inv; ri[2] = c02 * inv;
-    ri[3] = c01 * inv; ri[4] = c11 * inv; ri[5] = c12 * inv;
-    ri[6] = c02 * inv; ri[7] = c12 * inv; ri[8] = c22 * inv;
-  }
-  __syncthreads();
-  const bool iv = t < NI;
-  const int i = iv ? t : 0, k = i / 6, c = i % 6;
-  if (iv) {  // row c of B6 R'^-1 and of G_k (lower triangle)
-    double br[12];
-#pragma unroll
-    for (int l = 0; l < 4; ++l)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        const double* ri = ps.Ri[k][l];
-        double s;
-        if (c < 3) {
-          const double* bw = sm.Bw[k][c] + 3 * l;
-          s = (bw[0] * ri[b] + bw[1] * ri[3 + b]) + bw[2] * ri[6 + b];
-        } else {
-          s = dtm * ri[3 * (c - 3) + b];
-        }
-        br[3 * l + b] = s;
-      }
-#pragma unroll
-    for (int d = 0; d < 6; ++d) {
-      double s;
-      if (d < 3) {
-        const double* bw = sm.Bw[k][d];
-        s = 0.0;
-#pragma unroll
-        for (int j = 0; j < 12; ++j) s += br[j] * bw[j];
-      } else {
-        s = dtm * (((br[d - 3] + br[d]) + br[d + 3]) + br[d + 6]);
-      }
-      if (d <= c) ps.G[k][6 * c + d] = s;
-    }
-  }
-  __syncthreads();
-  double sii = 1.0;
-  if (iv) {  // Cholesky of G_k (schur_factor), the lane's column c of L, S_ii
-    double L[6][6];
-#pragma unroll
-    for (int r2 = 0; r2 < 6; ++r2)
-#pragma unroll
-      for (int c2 = 0; c2 < 6; ++c2) L[r2][c2] = 0.0;
-#pragma unroll
-    for (int cc = 0; cc < 6; ++cc) {
-      double s = ps.G[k][6 * cc + cc];
-#pragma unroll
-      for (int e = 0; e < cc; ++e) s -= L[cc][e] * L[cc][e];
-      const double dg = sqrt(s), dinv = recip(dg);
-      L[cc][cc] = dg;
-#pragma unroll
-      for (int r2 = cc + 1; r2 < 6; ++r2) {
-        double v = ps.G[k][6 * r2 + cc];
-#pragma unroll
-        for (int e = 0; e < cc; ++e) v -= L[r2][e] * L[cc][e];
-        L[r2][cc] = v * dinv;
-      }
-    }
-    double Lc[6];
-#pragma unroll
-    for (int e = 0; e < 6; ++e) {
-      double v = L[e][0];
-#pragma unroll
-      for (int cc = 1; cc < 6; ++cc) v = c == cc ? L[e][cc] : v;
-      Lc[e] = v;
-    }
-    double sv = 0.0, sw = 0.0;
-#pragma unroll
-    for (int e = 0; e < 6; ++e) {
-      const double v = sqrt(c_s * (2.0 * p.q_weights[6 + e])) * Lc[e];
-      double s = 0.0;
-#pragma unroll
-      for (int f = 0; f < 6; ++f) s += A.at(e, 6 + f) * Lc[f];
-      const double w = sqrt(c_s * (2.0 * p.q_weights[e])) * s;
-      sv += v * v;
-      sw += w * w;
-    }
-    sii = (1.0 + (double)(N - k) * sv) + alpha_jl(N, k, k) * sw;
-  }
-  return __syncthreads_or(iv && !(sii <= SCHUR_SMAX)) != 0;
-}
-
 // ---- KKT solve (every ADMM iteration) ------------------------------------------------------------
 // W[r]: w = D^-1 rhs in the variable layout; returns U[r] = (c B6'M B6 + R')^-1 w.
 template <int N, int R>

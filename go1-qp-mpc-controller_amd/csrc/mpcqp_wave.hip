@@ -68,8 +68,9 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   const int inst = blockIdx.x;
   if (inst >= batch) return;
   const int t = threadIdx.x;
-  // wave_kernel's hand-off counters start at zero (stream order): [0] rank-deficient feet, [1] an
-  // ill-conditioned Schur core at the initial rho (the pre-screen below), [2] one that crossed later
+  // wave_kernel's hand-off counters start at zero (stream order): [0] rank-deficient feet, [1]
+  // (unused: an ill-conditioned core at the initial rho, never seen; see the flag below), [2] an
+  // ill-conditioned Schur core after a rho update
   if (inst == 0 && t < 3) fb[t] = 0;
   {
     const double* rg = recs + (size_t)inst * C::REC;
@@ -573,22 +574,11 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     if (ws) out[SI::QN + j0] = sm.qn[j0];
   }
   for (int r = t; r < m; r += NTS) out[SI::E + r] = Ec[r];
-  // The Schur form's hand-off flag: 1 rank-deficient B6_k (the screen above), 2 an ill-conditioned
-  // Schur core at the initial rho (max S_ii of the first factorization above SCHUR_SMAX), 0 neither;
-  // wave_kernel<N, 1> solves flagged robots by the Riccati form from the start.
-  double flag = any_degen ? 1.0 : 0.0;
-  if constexpr (N <= 10) {
-    if (!any_degen) {  // (block-uniform)
-      __shared__ PrescreenScratch<N> ps;
-      const double rho0 = mode == 1 ? ws[WL::RHO] : dmin(dmax(p.rho, RHO_MIN), RHO_MAX);
-      double cont[4];
-#pragma unroll
-      for (int l = 0; l < 4; ++l) cont[l] = rec[MPCQP_REC_CONTACTS + l] != 0.0 ? 1.0 : 0.0;
-      if (schur_prescreen<N>(sm, ps, sm.Ap[0], sm.Ap[1], Dc, Ec, c_s, rho0, p, A, dtm, cont, rec[MPCQP_REC_FZMIN],
-                             rec[MPCQP_REC_FZMAX]))
-        flag = 2.0;
-    }
-  }
+  // The Schur form's hand-off flag: 1 for rank-deficient B6_k (the screen above).  (Evaluating max
+  // S_ii at the initial rho here as well was measured and dropped: at rho = 0.1 no C5 or heavy-weight
+  // robot crosses SCHUR_SMAX -- with OSQP's cost scaling S barely grows with the state weights; the
+  // crossings come after adapt_rho lowers rho -- and it cost scale_kernel 11 %, profiles/r05.)
+  const double flag = any_degen ? 1.0 : 0.0;
   if (t == 0) {
     out[SI::CS] = c_s;
     out[SI::MODE] = (double)mode;
@@ -637,9 +627,8 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
 // 1 = impulse-space Schur form (mpcqp_schur.h; N <= 10, nonnegative state weights).
 // The solve of robot `inst` by one wave (wave_kernel: one robot per workgroup).  Returns true when a
 // KS = 1 solve hands the robot to the Riccati form without having written anything: scale_kernel
-// flagged it (rank-deficient B6_k, or an ill-conditioned Schur core at the initial rho), or a later
-// factorization's max S_ii crossed SCHUR_SMAX; wave_kernel then solves it with KS = 0 in the same
-// wave.  fb[0..2] count the three cases.
+// flagged it (rank-deficient B6_k), or a factorization's max S_ii crossed SCHUR_SMAX; wave_kernel
+// then solves it with KS = 0 in the same wave.  fb[0] and fb[2] count the two cases.
 template <int N, int KS>
 __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, const double* __restrict__ recs,
                                            mpcqp_result* __restrict__ results, double* __restrict__ solution,
@@ -734,9 +723,9 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
     const double flag = im[SI::DEGEN];
     if (flag != 0.0) {
       // rank-deficient B6_k (collinear / coincident feet: G_k would be singular; the reference QP is
-      // still strictly convex, R > 0) or an ill-conditioned Schur core at the initial rho: the
-      // Riccati form (KS = 0) solves this robot.  Nothing of it has been written yet.
-      if (t == 0) atomicAdd(fb + (flag == 1.0 ? 0 : 1), 1);
+      // still strictly convex, R > 0): the Riccati form (KS = 0) solves this robot.  Nothing of it
+      // has been written yet.
+      if (t == 0) atomicAdd(fb, 1);
       return true;
     }
   }
@@ -1730,6 +1719,11 @@ static bool schur_ok(const mpcqp_params& p) {
 #endif
   return true;
 }
+// experiment builds: MPCQP_WAVE_LDS_PAD bytes of dynamic LDS per wave-kernel workgroup (fewer robots
+// per CU: per-robot phase costs without neighbours sharing the CU's LDS or instruction cache)
+#ifndef MPCQP_WAVE_LDS_PAD
+#define MPCQP_WAVE_LDS_PAD 0
+#endif
 template <int N>
 static hipError_t launch_wave(const LaunchArgs& a) {
   if (!a.fallback) return hipErrorInvalidValue;
@@ -1739,12 +1733,12 @@ static hipError_t launch_wave(const LaunchArgs& a) {
   if (e != hipSuccess) return e;
   if constexpr (N <= 10) {
     if (schur_ok(a.p)) {
-      hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs,
+      hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(a.batch), dim3(wv::NT), MPCQP_WAVE_LDS_PAD, (hipStream_t)a.stream, a.recs,
                          a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((wv::wave_kernel<N, 0>), dim3(a.batch), dim3(wv::NT), 0, (hipStream_t)a.stream, a.recs, a.batch,
+  hipLaunchKernelGGL((wv::wave_kernel<N, 0>), dim3(a.batch), dim3(wv::NT), MPCQP_WAVE_LDS_PAD, (hipStream_t)a.stream, a.recs, a.batch,
                      a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
   return hipGetLastError();
 }

@@ -59,7 +59,7 @@ class MpcQpSolver:
 
     def handoff_counts(self):
         """mpcqp_handoff_counts: robots of the last Schur-form solve that the Riccati form solved in
-        their own wave, as (rank-deficient feet, ill-conditioned at the initial rho, crossed later).
+        their own wave, as (rank-deficient feet, 0 (reserved), ill-conditioned after a rho update).
         Synchronizes the device."""
         import ctypes
         c = (ctypes.c_int32 * 3)()

@@ -26,9 +26,10 @@ int32_t mpcqp_abi_sizes(int32_t* params_size, int32_t* result_size);
 int32_t mpcqp_handle_slots(mpcqp_handle* h);
 
 /* Robots of the handle's last Schur-form (N <= 10) wave solve that the Riccati form solved in their
- * own wave: counts[0] rank-deficient feet, counts[1] an ill-conditioned Schur core at the initial
- * rho (scale_kernel's pre-screen, max S_ii > SCHUR_SMAX), counts[2] a core that crossed the
- * threshold after a rho update (left the Schur form at a check).  Synchronizes the device. */
+ * own wave: counts[0] rank-deficient feet (scale_kernel's screen), counts[1] always 0 (reserved: an
+ * ill-conditioned core at the initial rho, which the workloads never show), counts[2] a core whose
+ * max S_ii crossed SCHUR_SMAX after a rho update (it left the Schur form at the next check).
+ * Synchronizes the device. */
 int32_t mpcqp_handoff_counts(mpcqp_handle* h, int32_t counts[3]);
 
 /* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */

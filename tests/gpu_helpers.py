@@ -64,3 +64,14 @@ def sentinel(err, bound, label):
     if not os.environ.get("MPCQP_SENTINEL_CALIBRATE"):
         assert m <= bound, f"{label}: u0 error {m:.3e} above the regression sentinel {bound:.0e}"
     return m
+
+
+def note(label, **values):
+    """Prints a measurement and appends it to $MPCQP_SENTINEL_LOG (JSON lines) when set."""
+    import json
+    import os
+    print(f"[note] {label}: {values}")
+    log = os.environ.get("MPCQP_SENTINEL_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(json.dumps({"label": label, **values}) + "\n")

@@ -251,6 +251,9 @@ def test_cpp_terrain_adaptation_behind_compute_grf(oracle, tmp_path):
         subprocess.run(["make", "-C", os.path.join(REPO, "tests", "cpp")], check=True)
     T, B = 14, 4
     ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=47, gait="trot", swing_ticks=5)
+    for st in ticks:  # (the generator shares some arrays between ticks; each tick gets its own here)
+        st.root_euler_d = st.root_euler_d.copy()
+        st.root_pos = st.root_pos.copy()
     for t in (2, 3, 9):  # a low body: no terrain sample (:341-345)
         ticks[t].root_pos[1, 2] = 0.08
     rows = np.stack([mpcqp.pack_states(st) for st in ticks])

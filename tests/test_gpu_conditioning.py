@@ -1,9 +1,9 @@
 """Ill-conditioned Schur cores (mpcqp_schur.h, the hand-off): with four feet in contact and state
 weights a few times the Go1 defaults, S = I + L'CL gets large and the push-through identity
 R'^-1 w - B'(I - S^-1)B w loses digits (u0 off the oracle by up to 1e-3 at x 100, round-4 fuzz,
-profiles/r04/smax).  scale_kernel pre-screens max S_ii at the initial rho and wave_kernel solves such
-robots by the Riccati form from the start, in the same wave; a robot whose core crosses SCHUR_SMAX
-after a rho update leaves the Schur form at the next check and is solved again, also in its own wave.
+profiles/r04/smax).  A robot whose core crosses SCHUR_SMAX (after a rho update: at the initial rho
+none does) leaves the Schur form at the next check and is solved again by the Riccati form in its
+own wave (wave_kernel).
 Gates: status and iterations equal to the oracle, u0 within SURVEY §8(c)'s 1e-4, and a regression
 sentinel at the accuracy the hand-off achieves."""
 import numpy as np
@@ -11,7 +11,7 @@ import pytest
 import torch
 
 import mpcqp
-from gpu_helpers import rel_err_u0, sentinel, solve_gpu
+from gpu_helpers import note, rel_err_u0, sentinel, solve_gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -27,7 +27,7 @@ def test_heavy_state_weights_match_oracle(oracle, gait, scale):
     with mpcqp.MpcQpSolver(p) as s:
         got, _, _ = solve_gpu(s, recs)
         counts = s.handoff_counts()
-    print(f"hand-offs {gait} x{scale:g}: {counts}")
+    note(f"hand-offs {gait} x{scale:g}", counts=list(counts))
     ref = oracle.solve_batch(oracle.default_params(N, q=list(p.q_weights), r=list(p.r_weights)), recs, nthreads=8)
     np.testing.assert_array_equal(got["status"], ref["status"])
     np.testing.assert_array_equal(got["iters"], ref["iters"])
@@ -36,8 +36,8 @@ def test_heavy_state_weights_match_oracle(oracle, gait, scale):
     # regression sentinel: the hand-off keeps these within ~1e-6 (without it 1.4e-5 at x1 stance,
     # 4e-4 at x5, 1e-3 at x100)
     sentinel(err, 1e-5 if gait == "stance" or scale > 1 else 1e-8, f"conditioning {gait} x{scale:g}")
-    if gait == "stance" and scale >= 5:
-        assert counts[1] + counts[2] > 0  # the hand-off is exercised here
+    if gait == "stance":
+        assert counts[2] > 0  # the hand-off is exercised here
 
 
 @pytest.mark.parametrize("N", [3, 6, 10])
@@ -51,7 +51,7 @@ def test_heavy_weights_shorter_horizons(oracle, N):
     with mpcqp.MpcQpSolver(p) as s:
         got, _, _ = solve_gpu(s, recs)
         counts = s.handoff_counts()
-    print(f"hand-offs N={N}: {counts}")
+    note(f"hand-offs N={N} stance x20", counts=list(counts))
     ref = oracle.solve_batch(oracle.default_params(N, q=list(p.q_weights), r=list(p.r_weights)), recs, nthreads=8)
     np.testing.assert_array_equal(got["status"], ref["status"])
     np.testing.assert_array_equal(got["iters"], ref["iters"])
@@ -65,10 +65,11 @@ def test_heavy_weights_warm_ticks(oracle):
     sequence keep their warm slot (the Schur form writes nothing before it hands over; the Riccati
     form reads the previous tick's slot and writes this tick's)."""
     N, T, B = 10, 6, 48
-    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=7200, gait="trot", swing_ticks=2)
+    ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=7200, gait="trot", swing_ticks=3)
     recs_t = np.stack([mpcqp.assemble_compute_grf(s, N) for s in ticks])
+    recs_t[:, :, mpcqp._lib.REC_CONTACTS:mpcqp._lib.REC_CONTACTS + 4] = 1.0  # four feet down
     p0 = mpcqp.default_params(N)
-    p = mpcqp.default_params(N, q_weights=[w * 30.0 for w in p0.q_weights])
+    p = mpcqp.default_params(N, q_weights=[w * 100.0 for w in p0.q_weights])
     out = np.zeros((T, B), dtype=mpcqp.RESULT_DTYPE)
     handed = 0
     with mpcqp.MpcQpSolver(p) as s:
@@ -82,7 +83,7 @@ def test_heavy_weights_warm_ticks(oracle):
             out[t] = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=mpcqp.RESULT_DTYPE)
             c = s.handoff_counts()
             handed += c[1] + c[2]
-    print(f"warm ticks: {handed} hand-offs over {T} ticks")
+    note("hand-offs warm ticks stance x100", handed=handed, ticks=T, robots=B)
     op = oracle.default_params(N, q=list(p.q_weights), r=list(p.r_weights))
     ref = oracle.solve_sequence(op, recs_t, nthreads=8)
     worst = 0.0
@@ -92,30 +93,5 @@ def test_heavy_weights_warm_ticks(oracle):
         err = rel_err_u0(out[t]["u0"], ref[t]["u0"])
         assert np.all(err <= 1e-4), f"tick {t}"
         worst = max(worst, float(err.max()))
-    sentinel(np.array([worst]), 1e-5, "conditioning warm ticks x30")
+    sentinel(np.array([worst]), 1e-5, "conditioning warm ticks x100")
     assert handed > 0
-
-
-def test_prescreen_flag_in_scale_image(oracle):
-    """scale_kernel's image slot 56N + 2: 2 for a robot whose Schur core is ill-conditioned at the
-    initial rho (stance, heavy weights), 0 for the Go1-weight trot robots."""
-    N = 10
-    st = mpcqp.synthetic_go1(32, seed=7300, gait="stance")
-    recs = mpcqp.assemble_compute_grf(st, N)
-    p0 = mpcqp.default_params(N)
-    p = mpcqp.default_params(N, q_weights=[w * 100.0 for w in p0.q_weights])
-    with mpcqp.MpcQpSolver(p, debug=True) as s:
-        d_rec = torch.from_numpy(recs).cuda()
-        d_img = torch.zeros((32, s.scale_image_size), dtype=torch.float64, device="cuda")
-        s.scale_image_device(d_rec.data_ptr(), 32, 0, d_img.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        flag = d_img.cpu().numpy()[:, 56 * N + 2]
-    assert set(np.unique(flag)) <= {0.0, 2.0}
-    assert np.mean(flag == 2.0) > 0.5, flag
-    st2 = mpcqp.synthetic_go1(64, seed=7301, gait="trot")
-    with mpcqp.MpcQpSolver(mpcqp.default_params(N), debug=True) as s:
-        d_rec = torch.from_numpy(mpcqp.assemble_compute_grf(st2, N)).cuda()
-        d_img = torch.zeros((64, s.scale_image_size), dtype=torch.float64, device="cuda")
-        s.scale_image_device(d_rec.data_ptr(), 64, 0, d_img.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        assert np.all(d_img.cpu().numpy()[:, 56 * N + 2] == 0.0)

@@ -2,7 +2,7 @@
 G_k = B6_k R'^-1 B6_k', which is singular when the feet are coincident (e.g. all foot_pos_abs zero
 before the first kinematics update) or collinear — B6_k then has rank 3 or 5.  The reference QP is
 still strictly convex (R > 0) and OSQP solves it; scale_kernel screens every step's B6_k (Gram
-pivot ratio) and the engine hands such robots to the Riccati form (wave_fallback_kernel).  Gates: status and iteration count identical to the oracle, u0 within 1e-4
+pivot ratio) and the engine hands such robots to the Riccati form (in the same wave).  Gates: status and iteration count identical to the oracle, u0 within 1e-4
 relative, every force finite, and the non-degenerate robots of a mixed batch bit-identical to
 solving them without the degenerate ones."""
 import numpy as np
@@ -70,7 +70,7 @@ def test_degenerate_flag_in_scale_image(oracle, N):
 
 
 def test_degenerate_robots_in_a_large_batch(oracle):
-    """A 4096-robot C2 batch with 37 degenerate robots scattered through it: the fallback list
+    """A 4096-robot C2 batch with 37 degenerate robots scattered through it: the screen
     catches exactly those, the rest are untouched (bitwise equal to the batch without them)."""
     st = mpcqp.synthetic_go1(4096, seed=1000, gait="trot")
     recs = mpcqp.assemble_compute_grf(st, N)
@@ -79,7 +79,9 @@ def test_degenerate_robots_in_a_large_batch(oracle):
     mixed[idx] = _degenerate(recs[idx])
     with mpcqp.MpcQpSolver(mpcqp.default_params(N)) as s:
         clean, _, _ = solve_gpu(s, recs)
+        assert s.handoff_counts()[0] == 0
         got, _, _ = solve_gpu(s, mixed)
+        assert s.handoff_counts()[0] == idx.size  # exactly the degenerate robots took the Riccati form
     keep = np.setdiff1d(np.arange(4096), idx)
     for k in ("u0", "iters", "status", "rho_updates"):
         np.testing.assert_array_equal(got[k][keep], clean[k][keep])
@@ -91,7 +93,7 @@ def test_degenerate_robots_in_a_large_batch(oracle):
 
 def test_degenerate_feet_warm_ticks(oracle):
     """Warm-started ticks that start with zero feet (before the first kinematics update) and then
-    get real feet: the fallback carries the warm slot like the Schur form does."""
+    get real feet: the Riccati form carries the warm slot like the Schur form does."""
     T, B = 5, 16
     ticks = mpcqp.records.synthetic_go1_ticks(B, T, seed=61, gait="trot", swing_ticks=3)
     recs_t = np.stack([mpcqp.assemble_compute_grf(s, N) for s in ticks])

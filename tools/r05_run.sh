@@ -9,9 +9,13 @@ OUT=${1:?outdir}
 mkdir -p "$OUT"
 export MPCQP_SENTINEL_LOG="$PWD/$OUT/sentinels.jsonl"
 rm -f "$MPCQP_SENTINEL_LOG"
+rc=0
 timeout -k 10 400 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread \
-  > "$OUT/gpu_tests.txt" 2>&1 || { tail -30 "$OUT/gpu_tests.txt"; exit 1; }
-tail -2 "$OUT/gpu_tests.txt"
+  > "$OUT/gpu_tests.txt" 2>&1 || rc=$?
+grep -E "^FAILED|passed|failed" "$OUT/gpu_tests.txt" | tail -12
+# rc 1 = some tests failed (assertions): go on to the bench; anything else (a crash, abort, fault or
+# time limit) ends the call here
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
   -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-extras > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err"
@@ -42,3 +46,12 @@ for k, v in (d.get("extras") or {}).items():
 for r in csv.DictReader(open(o + "/trace/run_kernel_stats.csv")):
     print(r["Name"][:60], r["Calls"], r["AverageNs"])
 PY
+if [ "${CONTENTION:-0}" = 1 ]; then
+  bash tools/r05_contention.sh "$OUT/contention"
+fi
+if [ "${PMCSQ:-0}" = 1 ]; then
+  mkdir -p "$OUT/sq"
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_IFETCH \
+    --kernel-include-regex "wave_kernel" --output-format csv -d "$OUT/sq/p1" -o pmc \
+    -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-extras > /dev/null 2> "$OUT/sq/p1.err"
+fi

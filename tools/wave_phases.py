@@ -51,6 +51,10 @@ def main():
         for i, c in zip(ids, cyc):
             at.setdefault(i, []).append(c)
         ph["shader_ghz"].append((cyc[-1] - cyc[0]) / max(mk[-1, 2] - mk[0, 2], 1) * 0.1)
+        if 4 not in at:  # (MPCQP_PHASE_TIMING_ENDS builds: marks 0 and 20 only)
+            if 20 in at:
+                ph["total"].append(at[20][0] - at[0][0])
+            continue
         ph["setup"].append(at[4][0] - at[0][0])
         fac = [at[12][k] - at[10][k] for k in range(min(len(at[10]), len(at.get(12, []))))]
         ph["factor"] += fac
