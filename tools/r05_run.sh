@@ -55,3 +55,6 @@ if [ "${PMCSQ:-0}" = 1 ]; then
     --kernel-include-regex "wave_kernel" --output-format csv -d "$OUT/sq/p1" -o pmc \
     -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-extras > /dev/null 2> "$OUT/sq/p1.err"
 fi
+if [ "${MB:-0}" = 1 ]; then
+  timeout -k 10 60 tools/mb/mb_valu > "$OUT/mb_valu.txt" 2>&1 && cat "$OUT/mb_valu.txt"
+fi
