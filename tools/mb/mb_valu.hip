@@ -68,6 +68,28 @@ KERNEL(k_nop, B_NOP, 64)
   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x));
 KERNEL(k_max, B_MAX, 128)
 
+// DPP FMA patterns: accumulator count 1 / 2 / 4 with a distinct multiplier per instruction (the
+// mat-vec shape), and one accumulator with the same multiplier
+#define B_D1C asm volatile("s_nop 4\n\t" REP16(DG("%0", "%1", 0) DG("%0", "%2", 1) DG("%0", "%3", 2) DG("%0", "%4", 3) \
+  DG("%0", "%5", 4) DG("%0", "%6", 5) DG("%0", "%7", 6) DG("%0", "%9", 7)) \
+  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(g));
+#define DG(A, C, L) "v_fmac_f64_dpp " A ", %8, " C " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+KERNEL(k_d1c, B_D1C, 128)
+#define B_D2C asm volatile("s_nop 4\n\t" REP16(DG("%0", "%2", 0) DG("%1", "%3", 1) DG("%0", "%4", 2) DG("%1", "%5", 3) \
+  DG("%0", "%6", 4) DG("%1", "%7", 5) DG("%0", "%9", 6) DG("%1", "%9", 7)) \
+  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(g));
+KERNEL(k_d2c, B_D2C, 128)
+#define B_D4C asm volatile("s_nop 4\n\t" REP16(DG("%0", "%4", 0) DG("%1", "%5", 1) DG("%2", "%6", 2) DG("%3", "%7", 3) \
+  DG("%0", "%5", 4) DG("%1", "%6", 5) DG("%2", "%7", 6) DG("%3", "%9", 7)) \
+  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(g));
+KERNEL(k_d4c, B_D4C, 128)
+// plain FMA with a distinct multiplier per instruction, 4 accumulators
+#define PG(A, C) "v_fmac_f64 " A ", %8, " C "\n\t"
+#define B_P4C asm volatile(REP16(PG("%0", "%4") PG("%1", "%5") PG("%2", "%6") PG("%3", "%7") \
+  PG("%0", "%5") PG("%1", "%6") PG("%2", "%7") PG("%3", "%9")) \
+  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(g));
+KERNEL(k_p4c, B_P4C, 128)
+
 typedef void (*kfn)(double*, long long*, int);
 int main() {
   const int blocks = 1024, iters = 200;  // one 64-thread wave per SIMD on 256 CUs
@@ -83,7 +105,9 @@ int main() {
             {"v_fmac_f64 dep chain", k_chain, 128},       {"v_fmac_f64_dpp dep chain", k_dchain, 128},
             {"v_fmac_f64_dpp 3 acc rot", k_rot3, 96},    {"v_permlane16/32_swap", k_perm, 64},
             {"v_accvgpr write/read", k_acc, 64},          {"s_nop 1", k_nop, 64},
-            {"v_max/add_f64 x8 indep", k_max, 128}};
+            {"v_max/add_f64 x8 indep", k_max, 128},       {"dpp fma 1 acc, 8 mults", k_d1c, 128},
+            {"dpp fma 2 acc, 8 mults", k_d2c, 128},       {"dpp fma 4 acc, 8 mults", k_d4c, 128},
+            {"plain fma 4 acc, 8 mults", k_p4c, 128}};
   std::vector<long long> cyc(blocks);
   for (auto& k : ks) {
     hipLaunchKernelGGL(k.f, dim3(blocks), dim3(64), 0, 0, d_out, d_cyc, 2);
