@@ -950,18 +950,11 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
   double SRI[KS == 1 ? R : 1][3];
   (void)SRI;
   // KS = 1: P~v computed directly where the checks need it (mpcqp_schur.h schur_px)
-  auto px_of = [&](const double (&v)[R], double (&out)[R]) __attribute__((always_inline)) {
+  auto px_of = [&](const double (&v)[R], const double (&dd)[R], double (&out)[R]) __attribute__((always_inline)) {
     if constexpr (KS == 1) {
-      double dd[R], dvv[R];
+      double dvv[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-#ifdef MPCQP_XPXREG
-        dd[r] = DI[r];
-#else
-        dd[r] = dv_of(r);
-#endif
-        dvv[r] = dd[r] * v[r];
-      }
+      for (int r = 0; r < R; ++r) dvv[r] = dd[r] * v[r];
       schur_px<N, R>(sm, F, p, A, dtm, cost_c, Q2C, R2I, dvv, dd, vvr, out);
     }
   };
@@ -1389,9 +1382,31 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
     if (need_info) {
       // ---- update_info / check_termination / adapt_rho (osqp.c, auxil.c) ----
       // KS = 1: P~x of this iterate, local to the check (not carried through the loop)
+      // D and E of the lane's variables / rows.  The Riccati form loads them for the whole check in
+      // one batch (one memory round trip instead of one per round: C4 +1.4 %); the Schur form where
+      // they are used (holding them through P~x made its check slower: C2 -2 %, profiles/r05)
+      double DVc[R], EVc[R], E4c[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (KS == 0) {
+          DVc[r] = dv_of(r);
+          EVc[r] = ev_of(r);
+          E4c[r] = e4_of(r);
+        } else {
+          DVc[r] = EVc[r] = E4c[r] = 0.0;
+        }
+      }
+      auto dvc = [&](int r) __attribute__((always_inline)) { return KS == 0 ? DVc[r] : dv_of(r); };
+      auto evc = [&](int r) __attribute__((always_inline)) { return KS == 0 ? EVc[r] : ev_of(r); };
+      auto e4c = [&](int r) __attribute__((always_inline)) { return KS == 0 ? E4c[r] : e4_of(r); };
       double PXl[R];
       double (&PXc)[R] = KS == 1 ? PXl : PX;
-      if constexpr (KS == 1) px_of(X, PXc);
+      if constexpr (KS == 1) {
+        double dd[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) dd[r] = dv_of(r);
+        px_of(X, dd, PXc);
+      }
       if (tm_ck) WV_MARK(50);
       // The norms of update_info / check_termination / compute_rho_estimate, and the first-level
       // quantities of both infeasibility tests (||E dy||, the support term of dy, ||D dx||, q'dx:
@@ -1420,7 +1435,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
         const double xp = dpp<QP_PRIM>(X[r]), xz = dpp<QP_B2>(X[r]);
         const double ax = AK0[r] * xp + AK1[r] * xz, ax4 = AK4[r] * xz;
         const double aty = quad_at(Y[r], Y4[r], AK0[r], AK1[r], AK4[r], a);
-        const double evr = ev_of(r), e4r = e4_of(r);
+        const double evr = evc(r), e4r = e4c(r);
         if (kvr[r]) {
           const double ei = recip(evr), ei4 = recip(e4r);
           const double pr = ax + (-1.0) * Z[r], pr4 = ax4 + (-1.0) * Z4[r];
@@ -1448,7 +1463,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
         }
         // is_dual_infeasible: ||D dx||_inf and q~'dx
         if (vvr[r]) {
-          nx = nmax(nx, dabs(dv_of(r) * DX[r]));
+          nx = nmax(nx, dabs(dvc(r) * DX[r]));
           qd += Qv[r] * DX[r];
         }
       }
@@ -1483,7 +1498,12 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
         if (!dual_ok && ndx > DIV_TOL && qd < cost_c * eps_dinf * ndx) {
           // is_dual_infeasible (P~ delta_x = P~x_new - P~x_old)
           double pd = 0.0, PDX[R];
-          if constexpr (KS == 1) px_of(DX, PDX);
+          if constexpr (KS == 1) {
+            double dd[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) dd[r] = dv_of(r);
+            px_of(DX, dd, PDX);
+          }
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             if constexpr (KS == 0) PDX[r] = PX[r] - PXO[r];
@@ -1495,9 +1515,9 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
 #pragma unroll
             for (int r = 0; r < R; ++r) {
               const double dp = dpp<QP_PRIM>(DX[r]), dz = dpp<QP_B2>(DX[r]);
-              const double evr = ev_of(r);
+              const double evr = evc(r);
               const double v = (1.0 / evr) * (AK0[r] * dp + AK1[r] * dz);
-              const double v4 = (1.0 / e4_of(r)) * (AK4[r] * dz);
+              const double v4 = (1.0 / e4c(r)) * (AK4[r] * dz);
               const double lo = lo03(evr), hi = hi03(evr);
               if (kvr[r]) {
                 if ((hi < OSQP_INF * MIN_SCALING && v > eps_dinf * ndx) ||

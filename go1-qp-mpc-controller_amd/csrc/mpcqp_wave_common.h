@@ -127,6 +127,103 @@ struct WSmem {
 
 // ---- cross-lane primitives ---------------------------------------------------------------------
 #define WV_FM(A, M, L) "v_fmac_f64_dpp " A ", %[x], " M " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#ifndef MPCQP_MV_MULTI_ACC
+// y_i = sum_c M[i][c] x_c, x_c broadcast from lane 4(c/3)+c%3 of each DPP row, M row i in `c`.
+// One accumulator per mat-vec, the terms in column order: a dependent v_fmac_f64_dpp chain issues as
+// fast as independent ones for a lone wave (4.4 against 5.35 cycles, tools/mb/mb_valu), so rotating
+// accumulators only cost the zeroing moves and the closing adds (the round-4 form: MPCQP_MV_MULTI_ACC).
+#define WV_OPS12(P, C) [P##0] "v"(C[0]), [P##1] "v"(C[1]), [P##2] "v"(C[2]), [P##3] "v"(C[3]), [P##4] "v"(C[4]), \
+    [P##5] "v"(C[5]), [P##6] "v"(C[6]), [P##7] "v"(C[7]), [P##8] "v"(C[8]), [P##9] "v"(C[9]),                \
+    [P##10] "v"(C[10]), [P##11] "v"(C[11])
+#define WV_OPS6(P, C) [P##0] "v"(C[0]), [P##1] "v"(C[1]), [P##2] "v"(C[2]), [P##3] "v"(C[3]), [P##4] "v"(C[4]), \
+    [P##5] "v"(C[5])
+#define WV_M12(A) WV_FM(A, "%[c0]", 0) WV_FM(A, "%[c1]", 1) WV_FM(A, "%[c2]", 2) WV_FM(A, "%[c3]", 4)  \
+    WV_FM(A, "%[c4]", 5) WV_FM(A, "%[c5]", 6) WV_FM(A, "%[c6]", 8) WV_FM(A, "%[c7]", 9)                 \
+    WV_FM(A, "%[c8]", 10) WV_FM(A, "%[c9]", 12) WV_FM(A, "%[c10]", 13) WV_FM(A, "%[c11]", 14)
+#define WV_M6HI(A) WV_FM(A, "%[c0]", 8) WV_FM(A, "%[c1]", 9) WV_FM(A, "%[c2]", 10) WV_FM(A, "%[c3]", 12) \
+    WV_FM(A, "%[c4]", 13) WV_FM(A, "%[c5]", 14)
+#define WV_M6LO(A) WV_FM(A, "%[c0]", 0) WV_FM(A, "%[c1]", 1) WV_FM(A, "%[c2]", 2) WV_FM(A, "%[c3]", 4)  \
+    WV_FM(A, "%[c4]", 5) WV_FM(A, "%[c5]", 6)
+__device__ __forceinline__ double mv12(double x, const double (&c)[12]) {
+  double a = 0.0;
+  asm(WV_NOP_HEAD WV_M12("%[a]") : [a] "+&v"(a) : [x] "v"(x), WV_OPS12(c, c));
+  return a;
+}
+// sum over states 6..11 (lanes 8, 9, 10, 12, 13, 14) of c[s-6] x_s
+__device__ __forceinline__ double mv6(double x, const double (&c)[6]) {
+  double a = 0.0;
+  asm(WV_NOP_HEAD WV_M6HI("%[a]") : [a] "+&v"(a) : [x] "v"(x), WV_OPS6(c, c));
+  return a;
+}
+// Two / three independent mat-vecs interleaved in one block (each has its own x and rows)
+#define WV_FX(A, X, M, L) "v_fmac_f64_dpp " A ", " X ", " M " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#define WV_T2(L, I) WV_FX("%[a]", "%[x0]", "%[p" #I "]", L) WV_FX("%[b]", "%[x1]", "%[q" #I "]", L)
+#define WV_T3(L, I) WV_T2(L, I) WV_FX("%[d]", "%[x2]", "%[r" #I "]", L)
+__device__ __forceinline__ void mv12x2(double x0, double x1, const double (&c0)[12], const double (&c1)[12],
+                                       double& y0, double& y1) {
+  double a = 0.0, b = 0.0;
+  asm(WV_NOP_HEAD
+      WV_T2(0, 0) WV_T2(1, 1) WV_T2(2, 2) WV_T2(4, 3) WV_T2(5, 4) WV_T2(6, 5)
+      WV_T2(8, 6) WV_T2(9, 7) WV_T2(10, 8) WV_T2(12, 9) WV_T2(13, 10) WV_T2(14, 11)
+      : [a] "+&v"(a), [b] "+&v"(b)
+      : [x0] "v"(x0), [x1] "v"(x1), WV_OPS12(p, c0), WV_OPS12(q, c1));
+  y0 = a;
+  y1 = b;
+}
+__device__ __forceinline__ void mv12x3(double x0, double x1, double x2, const double (&c0)[12],
+                                       const double (&c1)[12], const double (&c2)[12], double& y0, double& y1,
+                                       double& y2) {
+  double a = 0.0, b = 0.0, d = 0.0;
+  asm(WV_NOP_HEAD
+      WV_T3(0, 0) WV_T3(1, 1) WV_T3(2, 2) WV_T3(4, 3) WV_T3(5, 4) WV_T3(6, 5)
+      WV_T3(8, 6) WV_T3(9, 7) WV_T3(10, 8) WV_T3(12, 9) WV_T3(13, 10) WV_T3(14, 11)
+      : [a] "+&v"(a), [b] "+&v"(b), [d] "+&v"(d)
+      : [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), WV_OPS12(p, c0), WV_OPS12(q, c1), WV_OPS12(r, c2));
+  y0 = a;
+  y1 = b;
+  y2 = d;
+}
+#undef WV_T2
+#undef WV_T3
+#undef WV_FX
+// y[r] = M_r x[r] for the R register rounds of a parallel phase, interleaved.
+template <int R>
+__device__ __forceinline__ void mv_rounds(const double (&x)[R], const double (&c)[R][12], double (&y)[R]) {
+  if constexpr (R == 1) {
+    y[0] = mv12(x[0], c[0]);
+  } else if constexpr (R == 2) {
+    mv12x2(x[0], x[1], c[0], c[1], y[0], y[1]);
+  } else if constexpr (R == 3) {
+    mv12x3(x[0], x[1], x[2], c[0], c[1], c[2], y[0], y[1], y[2]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) y[r] = mv12(x[r], c[r]);
+  }
+}
+// init + sum_c M[c] x_c: the chains' "- a_k" / "+ h_k" as the accumulator's start
+__device__ __forceinline__ double mv12a(double x, const double (&c)[12], double init) {
+  double a = init;
+  asm(WV_NOP_HEAD WV_M12("%[a]") : [a] "+&v"(a) : [x] "v"(x), WV_OPS12(c, c));
+  return a;
+}
+// init + sum over states 6..11 (lanes 8, 9, 10, 12, 13, 14) of c[s-6] x_s
+__device__ __forceinline__ double mv6a(double x, const double (&c)[6], double init) {
+  double a = init;
+  asm(WV_NOP_HEAD WV_M6HI("%[a]") : [a] "+&v"(a) : [x] "v"(x), WV_OPS6(c, c));
+  return a;
+}
+// init + sum over states 0..5 (lanes 0, 1, 2, 4, 5, 6) of c[s] x_s
+__device__ __forceinline__ double mv6lo_a(double x, const double (&c)[6], double init) {
+  double a = init;
+  asm(WV_NOP_HEAD WV_M6LO("%[a]") : [a] "+&v"(a) : [x] "v"(x), WV_OPS6(c, c));
+  return a;
+}
+#undef WV_OPS12
+#undef WV_OPS6
+#undef WV_M12
+#undef WV_M6HI
+#undef WV_M6LO
+#else
 // y_i = sum_c M[i][c] x_c, x_c broadcast from lane 4(c/3)+c%3 of each DPP row, M row i in `c`.
 // Hazards (the compiler cannot see into the asm): a DPP instruction needs 2 wait states after a
 // VALU write of ANY of its VGPR operands and 5 after an EXEC write.  Hence the leading s_nop 4 and
@@ -243,6 +340,7 @@ __device__ __forceinline__ double mv6lo_a(double x, const double (&c)[6], double
   return (a1 + a2) + a0;
 }
 
+#endif  // MPCQP_MV_MULTI_ACC
 #undef WV_FM
 
 // quad_perm DPP of a double
