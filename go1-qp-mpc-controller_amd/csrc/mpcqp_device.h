@@ -6,6 +6,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/mpcqp.h"
 #include "mpcqp_internal.h"
 
@@ -173,6 +175,36 @@ __device__ __forceinline__ double wave_nmax(double v) {
   v = nmax(v, dpp<0xB1>(v));
   v = swap16_reduce(v, op);
   return swap32_reduce(v, op);
+}
+
+// KM max-reductions (non-negative operands, as wave_nmax) and KS sum-reductions (as wave_sum) of one
+// wave, level by level: every value takes exactly the operations of its single reduction, in the same
+// order (bitwise the same results), but the values of a level are independent, so each DPP read of a
+// value comes several instructions after the VALU write that made it (no wait states, which a lone
+// chain needs at every level: 2 states = s_nop 1, 8.4 cycles).
+template <int KM, int KS>
+__device__ __forceinline__ void wave_reduce_batch(double (&mx)[KM], double (&sm)[KS]) {
+  auto level = [&](auto CTRL) __attribute__((always_inline)) {
+    constexpr int ctrl = decltype(CTRL)::value;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) mx[k] = nmax(mx[k], dpp<ctrl>(mx[k]));
+#pragma unroll
+    for (int k = 0; k < KS; ++k) sm[k] = sm[k] + dpp<ctrl>(sm[k]);
+  };
+  level(std::integral_constant<int, 0x140>{});
+  level(std::integral_constant<int, 0x141>{});
+  level(std::integral_constant<int, 0x4E>{});
+  level(std::integral_constant<int, 0xB1>{});
+  auto mop = [](double a, double b) __attribute__((always_inline)) { return nmax(a, b); };
+  auto sop = [](double a, double b) __attribute__((always_inline)) { return a + b; };
+#pragma unroll
+  for (int k = 0; k < KM; ++k) mx[k] = swap16_reduce(mx[k], mop);
+#pragma unroll
+  for (int k = 0; k < KS; ++k) sm[k] = swap16_reduce(sm[k], sop);
+#pragma unroll
+  for (int k = 0; k < KM; ++k) mx[k] = swap32_reduce(mx[k], mop);
+#pragma unroll
+  for (int k = 0; k < KS; ++k) sm[k] = swap32_reduce(sm[k], sop);
 }
 
 // ---- condensation: ConvexMpc.cpp:110-245 ----------------------------------------------------

@@ -1404,7 +1404,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
       if constexpr (KS == 1) {
         double dd[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) dd[r] = dv_of(r);
+        for (int r = 0; r < R; ++r) dd[r] = dvc(r);
         px_of(X, dd, PXc);
       }
       if (tm_ck) WV_MARK(50);
@@ -1467,11 +1467,18 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
           qd += Qv[r] * DX[r];
         }
       }
+      // the 10 max- and 2 sum-reductions level by level (wave_reduce_batch: same bits, no waits)
+      double rm[NM + 2], rs[2] = {lh, qd};
 #pragma unroll
-      for (int k = 0; k < NM; ++k) mx[k] = wave_nmax(mx[k]);
-      const double ndy = wave_nmax(nd), ndx = wave_nmax(nx);
-      lh = wave_sum(lh);
-      qd = wave_sum(qd);
+      for (int k = 0; k < NM; ++k) rm[k] = mx[k];
+      rm[NM] = nd;
+      rm[NM + 1] = nx;
+      wave_reduce_batch(rm, rs);
+#pragma unroll
+      for (int k = 0; k < NM; ++k) mx[k] = rm[k];
+      const double ndy = rm[NM], ndx = rm[NM + 1];
+      lh = rs[0];
+      qd = rs[1];
       pri_res = mx[0];
       dua_res = cinv * mx[4];
       iters = iter;
@@ -1501,7 +1508,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
           if constexpr (KS == 1) {
             double dd[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) dd[r] = dv_of(r);
+            for (int r = 0; r < R; ++r) dd[r] = dvc(r);
             px_of(DX, dd, PDX);
           }
 #pragma unroll
