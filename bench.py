@@ -320,6 +320,12 @@ def run_rank(args):
                 "bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS, "traffic": load_traffic(key, eff_name),
                 "kernel": eff_name, "kernel_ms": kern_ms, "algorithmic_flop_per_launch": flops,
+                "parts": solver.split_parts(Bl),
+                "kernel_ms_what": ("span of one solve call on the caller's stream (HIP events): the batch's "
+                                   "scale_kernel + wave_kernel pairs, split into `parts` concurrent parts on the "
+                                   "handle's internal streams; a rocprofv3 kernel trace gives the same span as "
+                                   "the first launch's start to the last launch's end of each step "
+                                   "(tools/trace_span.py)"),
                 "note": ("binary64 on the VALU (v_fmac_f64 DPP): "
                          + ("impulse-space Schur-form KKT solve (one dense 6N x 6N mat-vec per ADMM "
                             "iteration, in-register Gauss-Jordan per rho)" if N <= 10 else

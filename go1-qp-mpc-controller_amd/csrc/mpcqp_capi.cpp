@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -22,7 +23,17 @@ struct mpcqp_handle {
   double* work = nullptr;    // per-robot 12N x 16*ceil(12N/16) binary64 workspace (scaled Hessian)
   size_t work_cap = 0;       // instances the workspace can hold
   size_t work_per = 0;       // doubles per instance the workspace was sized for
-  int* fb = nullptr;         // wave path: the Schur -> Riccati hand-off counters of the last solve [4] ints
+  int* fb = nullptr;         // wave path: Schur -> Riccati hand-off counters, [4] ints per batch part
+  // The wave path splits a batch into parts solved concurrently on internal streams (forked from
+  // and joined to the caller's stream by events): one part's scale_kernel runs beside another
+  // part's wave_kernel and the parts' dispatch tails interleave (split_parts; tools/split_exp.py,
+  // profiles/r05/split).  Results are bitwise those of one launch.
+  static constexpr int KMAX = 8;
+  int split = 0;             // parts per solve: 0 = auto (split_parts), else MPCQP_SPLIT / mpcqp_set_split
+  int fb_parts = 1;          // parts of the last solve (hand-off counters to sum)
+  hipStream_t sub[KMAX] = {};
+  hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_join[KMAX] = {};
   int path = 0;              // 0 auto (= 3), 3 Riccati wave; debug library only: 1 dense K^-1, 2 Riccati workgroup
   // host wrapper: device buffers, a private stream and two pinned staging chunks
   hipStream_t hstream = nullptr;
@@ -111,10 +122,34 @@ hipError_t ensure_workspace(mpcqp_handle* h, int32_t batch, void* stream) {
   h->work_cap = 0;
   h->work_per = 0;
   if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(double) * per * cap);
-  if (e == hipSuccess) e = hipMalloc(&h->fb, sizeof(int) * 4);
+  if (e == hipSuccess) e = hipMalloc(&h->fb, sizeof(int) * 4 * mpcqp_handle::KMAX);
+  if (e == hipSuccess) e = hipMemset(h->fb, 0, sizeof(int) * 4 * mpcqp_handle::KMAX);
   if (e == hipSuccess) {
     h->work_cap = cap;
     h->work_per = per;
+  }
+  return e;
+}
+
+// Parts a wave-path solve of `batch` robots is split into.  Auto: three from 3072 robots, two from
+// 2048 (measured, tools/split_exp.py, profiles/r05/split: three parts C2 1.630 -> 1.582 ms, C5
+// 3.186 -> 2.971 ms, C4 5.44 -> 5.26 ms, C3's 8192-robot shard and 65536 robots unchanged; four
+// parts are slower everywhere: the caller's stream plus three internal ones already fill the
+// process's four hardware queues, and a fifth stream shares one in order).
+int split_parts(const mpcqp_handle* h, int32_t batch) {
+  int k = h->split > 0 ? h->split : (batch >= 3072 ? 3 : batch >= 2048 ? 2 : 1);
+  if (k > mpcqp_handle::KMAX) k = mpcqp_handle::KMAX;
+  if (k > batch) k = batch;
+  return k < 1 ? 1 : k;
+}
+
+// The internal streams and events of the batch split, created once per handle.
+hipError_t ensure_split_streams(mpcqp_handle* h) {
+  hipError_t e = hipSuccess;
+  if (!h->ev_fork) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+  for (int i = 0; i < mpcqp_handle::KMAX && e == hipSuccess; ++i) {
+    if (!h->sub[i]) e = hipStreamCreateWithFlags(&h->sub[i], hipStreamNonBlocking);
+    if (e == hipSuccess && !h->ev_join[i]) e = hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming);
   }
   return e;
 }
@@ -243,6 +278,9 @@ int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** 
   if (per_cu < 1) per_cu = 1;
   h->slots = cus * per_cu;
   h->cus = cus;
+  if (const char* sp = getenv("MPCQP_SPLIT")) h->split = atoi(sp);
+  e = ensure_split_streams(h);
+  if (e != hipSuccess) { mpcqp_destroy(h); return MPCQP_ERR_HIP; }
   *out = h;
   return MPCQP_OK;
 }
@@ -263,6 +301,12 @@ int32_t mpcqp_destroy(mpcqp_handle* h) {
     (void)hipHostFree(h->pin[i]);
   }
   if (h->hstream) (void)hipStreamDestroy(h->hstream);
+  for (int i = 0; i < mpcqp_handle::KMAX; ++i) {
+    if (h->sub[i]) (void)hipStreamSynchronize(h->sub[i]);
+    if (h->sub[i]) (void)hipStreamDestroy(h->sub[i]);
+    if (h->ev_join[i]) (void)hipEventDestroy(h->ev_join[i]);
+  }
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   delete h;
   return MPCQP_OK;
 }
@@ -297,7 +341,46 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
     case 1: e = mpcqp::launch_solve_any(a); break;
     case 2: e = mpcqp::launch_riccati_any(a); break;
 #endif
-    default: e = mpcqp::launch_wave_any(a); break;
+    default: {
+      const int parts = split_parts(h, batch);
+      h->fb_parts = parts;
+      if (parts == 1) {
+        e = mpcqp::launch_wave_any(a);
+        break;
+      }
+      // fork: part 0 runs on the caller's stream, every other part on an internal stream that waits
+      // for the work queued on the caller's stream so far (parts + 0 streams more: a process has
+      // few hardware queues, GPU_MAX_HW_QUEUES = 4, and streams beyond them share one in order)
+      e = hipEventRecord(h->ev_fork, (hipStream_t)stream);
+      const size_t rs = (size_t)MPCQP_REC_SIZE(h->p.horizon), n = (size_t)MPCQP_NUM_DOF * h->p.horizon;
+      const size_t ws = (size_t)mpcqp::warm_state_doubles(h->p.horizon);
+      for (int i = 0; i < parts && e == hipSuccess; ++i) {
+        const int b0 = (int)((int64_t)batch * i / parts), b1 = (int)((int64_t)batch * (i + 1) / parts);
+        mpcqp::LaunchArgs ai = a;
+        ai.recs = d_records + rs * b0;
+        ai.batch = b1 - b0;
+        ai.grid = b1 - b0;
+        ai.results = d_results + b0;
+        ai.solution = d_solution ? d_solution + n * b0 : nullptr;
+        ai.work = h->work + h->work_per * b0;
+        ai.trace = d_trace ? d_trace + (size_t)b0 * MPCQP_TRACE_LEN * 4 : nullptr;
+        ai.trace_cap = d_trace && trace_cap > b0 ? trace_cap - b0 : 0;
+        ai.wstate = d_state ? d_state + ws * b0 : nullptr;
+        ai.fallback = h->fb + 4 * i;
+        if (i == 0) {
+          ai.stream = stream;
+          e = mpcqp::launch_wave_any(ai);
+          continue;
+        }
+        ai.stream = h->sub[i];
+        e = hipStreamWaitEvent(h->sub[i], h->ev_fork, 0);
+        if (e == hipSuccess) e = mpcqp::launch_wave_any(ai);
+        if (e == hipSuccess) e = hipEventRecord(h->ev_join[i], h->sub[i]);
+      }
+      // join: the caller's stream waits for every other part
+      for (int i = 1; i < parts && e == hipSuccess; ++i) e = hipStreamWaitEvent((hipStream_t)stream, h->ev_join[i], 0);
+      break;
+    }
   }
   if (e != hipSuccess) return set_hip_error(h, e, "solve_kernel launch");
   return MPCQP_OK;
@@ -513,8 +596,23 @@ int32_t mpcqp_handoff_counts(mpcqp_handle* h, int32_t counts[3]) {
   DeviceGuard g(h->device);
   hipError_t e = g.err;
   if (e == hipSuccess) e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemcpy(counts, h->fb, sizeof(int32_t) * 3, hipMemcpyDeviceToHost);
+  int32_t all[4 * mpcqp_handle::KMAX];
+  if (e == hipSuccess) e = hipMemcpy(all, h->fb, sizeof(int32_t) * 4 * h->fb_parts, hipMemcpyDeviceToHost);
+  for (int i = 0; i < h->fb_parts && e == hipSuccess; ++i)
+    for (int j = 0; j < 3; ++j) counts[j] += all[4 * i + j];
   return e == hipSuccess ? MPCQP_OK : set_hip_error(h, e, "mpcqp_handoff_counts");
+}
+
+int32_t mpcqp_debug_set_split(mpcqp_handle* h, int32_t parts) {
+  if (!h || parts < 0 || parts > mpcqp_handle::KMAX) return -MPCQP_ERR_INVALID_ARG;
+  const int32_t old = h->split;
+  h->split = parts;
+  return old;
+}
+
+int32_t mpcqp_debug_split_parts(mpcqp_handle* h, int32_t batch) {
+  if (!h || batch < 1) return 0;
+  return effective_path(h) == 3 ? split_parts(h, batch) : 1;
 }
 
 int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {

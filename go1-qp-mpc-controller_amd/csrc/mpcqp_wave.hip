@@ -1081,6 +1081,16 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
             bcur[5] = a == 2 ? -dtm : 0.0;
           }
           __builtin_amdgcn_sched_barrier(0);
+#ifndef MPCQP_CHAIN_SPLIT
+          if constexpr (k >= 1 && k < N - 1) {  // a middle step: one block (chain_bwd)
+            const double m = rmove2<row_of(k + 1), row_of(k)>(cur);
+            double tk = W[r], sn = m;
+            chain_bwd(m, bcur, CAT, kcur, tk, sn);
+            TT[r] = (q == row_of(k)) ? tk : TT[r];
+            cur = sn;
+            return;
+          }
+#endif
           double m = 0.0, tk = W[r];
           if constexpr (k < N - 1) {
             m = rmove2<row_of(k + 1), row_of(k)>(cur);
@@ -1132,6 +1142,18 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
             }
           }
           __builtin_amdgcn_sched_barrier(0);
+#ifndef MPCQP_CHAIN_SPLIT
+          if constexpr (k >= 1 && k <= N - 2) {  // a middle step: one block (chain_fwd)
+            const double m = rmove2<row_of(k - 1), row_of(k)>(cur);
+            double nu = -G[r], ax = m, hb = 0.0;
+            chain_fwd(m, kcur, CAX, bcu, nu, ax, hb);
+            U[r] = (q == row_of(k)) ? -nu : U[r];
+            const double ls = dtm * legsum(nu);
+            const double bnu = leg == 2 ? hb : (leg == 3 ? ls : 0.0);
+            cur = ax - bnu;
+            return;
+          }
+#endif
           double m = 0.0, nu = -G[r];  // nu = -u_k = K_k x_k - g_k
           if constexpr (k >= 1) {
             m = rmove2<row_of(k - 1), row_of(k)>(cur);

@@ -218,6 +218,44 @@ __device__ __forceinline__ double mv6lo_a(double x, const double (&c)[6], double
   asm(WV_NOP_HEAD WV_M6LO("%[a]") : [a] "+&v"(a) : [x] "v"(x), WV_OPS6(c, c));
   return a;
 }
+// One middle step of each chain of the Acl-free Riccati form (N > 12) in one block, so that the
+// step's wait states come from its own independent FMAs instead of s_nop (8.4 cycles for 2 states):
+// only m, the row-moved chain value, is a fresh VALU result at the block's start.  Every accumulator
+// takes the same FMAs in the same order as the separate helpers (bitwise the same results).
+//   backward: tk = w + sum_hi bcast(m) bc (mv6a);  s = m + sum_lo bcast(m) cat (mv6lo_a), then
+//             s += sum bcast(tk) kc (mv12a(tk, kc, s)): s is the chain's next value
+//   forward:  nu = -g + sum bcast(m) kc (mv12a);  ax = m + sum_hi bcast(m) cax (mv6a);
+//             hb = sum bcast(nu) bc (mv12)
+#define WV_FY(A, X, M, L) "v_fmac_f64_dpp %[" A "], %[" X "], %[" M "] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ void chain_bwd(double m, const double (&bc)[6], const double (&cat)[6],
+                                          const double (&kc)[12], double& tk, double& s) {
+  asm(WV_NOP_HEAD
+      WV_FY("t", "m", "b0", 8) WV_FY("s", "m", "a0", 0) WV_FY("t", "m", "b1", 9) WV_FY("s", "m", "a1", 1)
+      WV_FY("t", "m", "b2", 10) WV_FY("s", "m", "a2", 2) WV_FY("t", "m", "b3", 12) WV_FY("s", "m", "a3", 4)
+      WV_FY("t", "m", "b4", 13) WV_FY("t", "m", "b5", 14) WV_FY("s", "m", "a4", 5) WV_FY("s", "m", "a5", 6)
+      // (tk's last write is two instructions back)
+      WV_FY("s", "t", "k0", 0) WV_FY("s", "t", "k1", 1) WV_FY("s", "t", "k2", 2) WV_FY("s", "t", "k3", 4)
+      WV_FY("s", "t", "k4", 5) WV_FY("s", "t", "k5", 6) WV_FY("s", "t", "k6", 8) WV_FY("s", "t", "k7", 9)
+      WV_FY("s", "t", "k8", 10) WV_FY("s", "t", "k9", 12) WV_FY("s", "t", "k10", 13) WV_FY("s", "t", "k11", 14)
+      : [t] "+&v"(tk), [s] "+&v"(s)
+      : [m] "v"(m), WV_OPS6(b, bc), WV_OPS6(a, cat), WV_OPS12(k, kc));
+}
+__device__ __forceinline__ void chain_fwd(double m, const double (&kc)[12], const double (&cax)[6],
+                                          const double (&bc)[12], double& nu, double& ax, double& hb) {
+  asm(WV_NOP_HEAD
+      WV_FY("n", "m", "k0", 0) WV_FY("x", "m", "c0", 8) WV_FY("n", "m", "k1", 1) WV_FY("x", "m", "c1", 9)
+      WV_FY("n", "m", "k2", 2) WV_FY("x", "m", "c2", 10) WV_FY("n", "m", "k3", 4) WV_FY("x", "m", "c3", 12)
+      WV_FY("n", "m", "k4", 5) WV_FY("n", "m", "k5", 6) WV_FY("n", "m", "k6", 8) WV_FY("n", "m", "k7", 9)
+      WV_FY("n", "m", "k8", 10) WV_FY("n", "m", "k9", 12) WV_FY("n", "m", "k10", 13) WV_FY("n", "m", "k11", 14)
+      WV_FY("x", "m", "c4", 13) WV_FY("x", "m", "c5", 14)
+      // (nu's last write is two instructions back)
+      WV_FY("h", "n", "d0", 0) WV_FY("h", "n", "d1", 1) WV_FY("h", "n", "d2", 2) WV_FY("h", "n", "d3", 4)
+      WV_FY("h", "n", "d4", 5) WV_FY("h", "n", "d5", 6) WV_FY("h", "n", "d6", 8) WV_FY("h", "n", "d7", 9)
+      WV_FY("h", "n", "d8", 10) WV_FY("h", "n", "d9", 12) WV_FY("h", "n", "d10", 13) WV_FY("h", "n", "d11", 14)
+      : [n] "+&v"(nu), [x] "+&v"(ax), [h] "+&v"(hb)
+      : [m] "v"(m), WV_OPS12(k, kc), WV_OPS6(c, cax), WV_OPS12(d, bc));
+}
+#undef WV_FY
 #undef WV_OPS12
 #undef WV_OPS6
 #undef WV_M12

@@ -57,6 +57,18 @@ class MpcQpSolver:
     def reserve(self, batch):
         check(self._L.mpcqp_reserve(self._h, int(batch)), self._h, "mpcqp_reserve", self._L)
 
+    def set_split(self, parts):
+        """mpcqp_debug_set_split: parts a solve is split into over the handle's internal streams
+        (0 auto, 1 one launch, up to 8).  Returns the previous setting."""
+        old = int(self._L.mpcqp_debug_set_split(self._h, int(parts)))
+        if old < 0:
+            raise ValueError("mpcqp_debug_set_split: parts must be 0..8")
+        return old
+
+    def split_parts(self, batch):
+        """mpcqp_debug_split_parts: parts a solve of `batch` robots is split into."""
+        return int(self._L.mpcqp_debug_split_parts(self._h, int(batch)))
+
     def handoff_counts(self):
         """mpcqp_handoff_counts: robots of the last Schur-form solve that the Riccati form solved in
         their own wave, as (rank-deficient feet, 0 (reserved), ill-conditioned after a rho update).

@@ -32,6 +32,16 @@ int32_t mpcqp_handle_slots(mpcqp_handle* h);
  * Synchronizes the device. */
 int32_t mpcqp_handoff_counts(mpcqp_handle* h, int32_t counts[3]);
 
+/* Parts a wave-path solve is split into (solved concurrently on the handle's internal streams,
+ * forked from and joined to the caller's stream; results are bitwise those of one launch):
+ * 0 = auto (3 parts from 3072 robots, 2 from 2048), 1 = one launch, up to 8.  The environment
+ * variable MPCQP_SPLIT sets the initial value at mpcqp_create.  Returns the previous setting, or
+ * -MPCQP_ERR_INVALID_ARG. */
+int32_t mpcqp_debug_set_split(mpcqp_handle* h, int32_t parts);
+
+/* Parts a solve of `batch` robots on this handle is split into under its current setting. */
+int32_t mpcqp_debug_split_parts(mpcqp_handle* h, int32_t batch);
+
 /* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */
 int32_t mpcqp_solve_threads(int32_t horizon);
 

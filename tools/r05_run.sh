@@ -46,6 +46,8 @@ for k, v in (d.get("extras") or {}).items():
 for r in csv.DictReader(open(o + "/trace/run_kernel_stats.csv")):
     print(r["Name"][:60], r["Calls"], r["AverageNs"])
 PY
+python3 tools/trace_span.py "$OUT/trace/run_kernel_trace.csv" | tee "$OUT/trace_span.json"
+python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print('bench under rocprof: kernel_ms', r['kernel_ms'], 'parts', r.get('parts'))" "$OUT/bench_under_rocprof.json"
 if [ "${CONTENTION:-0}" = 1 ]; then
   bash tools/r05_contention.sh "$OUT/contention"
 fi
