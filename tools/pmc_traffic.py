@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--key", default="N10_B4096_trot")
     ap.add_argument("--kernel", default="scale_kernel,wave_kernel",
                     help="comma-separated kernel-name substrings; per-launch means are summed (one solve)")
+    ap.add_argument("--parts", type=int, default=1,
+                    help="launches of each kernel per solve (the wave path's batch split): the per-dispatch "
+                         "means are multiplied by it, so the entry is per solve")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     kernels = [k for k in a.kernel.split(",") if k]
@@ -71,16 +74,18 @@ def main():
         write_kib += w_kib
         knames.append(sorted(set(names.values()))[0])
         ndisp.append(min(nf, nw))
-    fetch_b = fetch_kib * 1024.0 * 2.0  # gfx950: FETCH_SIZE counts half of the bytes
-    write_b = write_kib * 1024.0
+    fetch_b = fetch_kib * 1024.0 * 2.0 * a.parts  # gfx950: FETCH_SIZE counts half of the bytes
+    write_b = write_kib * 1024.0 * a.parts
     entry = {
         "kernel": " + ".join(knames),
         "dispatches": min(ndisp),
-        "fetch_size_kib_raw": fetch_kib,
-        "write_size_kib_raw": write_kib,
+        "fetch_size_kib_raw_per_dispatch": fetch_kib,
+        "write_size_kib_raw_per_dispatch": write_kib,
         "fetch_bytes_corrected": fetch_b,
         "write_bytes": write_b,
         "hbm_bytes_per_launch": fetch_b + write_b,
+        "parts": a.parts,
+        "per": "one solve call (the per-dispatch means of each kernel times `parts`)",
         "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads), KiB -> B; other widths uncalibrated",
     }
     data = {}
