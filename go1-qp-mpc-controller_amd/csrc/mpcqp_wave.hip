@@ -1029,6 +1029,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
 
     // ---- KKT solve: u = (c B'Q̄B + R')^-1 D^-1 rhs, x~ = D^-1 u ----
     double U[R];
+    auto kkt = [&]() __attribute__((always_inline)) {
     const bool tm_it = iter == 60;
     if (tm_it) WV_MARK(40);
     if constexpr (KS == 1) {
@@ -1338,17 +1339,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
 #endif
     }
     if (tm_it) WV_MARK(45);
-    bool is_check = false, is_adapt = false;
-    if (p.check_termination && --to_check == 0) {
-      is_check = true;
-      to_check = p.check_termination;
-    }
-    if (p.adaptive_rho && --to_adapt == 0) {
-      is_adapt = true;
-      to_adapt = p.adaptive_rho_interval;
-    }
-    const bool last = iter == p.max_iter;
-    const bool need_info = is_check || is_adapt || last;
+    };  // kkt
 
     // ---- update_x / update_z / update_y, and P~x by the KKT identity P~x~ = rhs - sigma x~ - A~'rho A~x~
     // this iteration's deltas, for the infeasibility tests of a need_info iteration only
@@ -1395,6 +1386,40 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
       RHS[r] = (sigma * X[r] - Qv[r]) + at;
     }
     };
+
+#ifndef MPCQP_SINGLE_LOOP
+    // The iterations before the next one that needs update_info (a termination check, an adapt_rho
+    // step or the last iteration) run in a loop of their own: the check's registers are then live
+    // only outside it, and the allocator keeps the ADMM state of the inner loop in registers.
+    {
+      int plain = p.max_iter - iter;
+      if (p.check_termination) plain = min(plain, to_check - 1);
+      if (p.adaptive_rho) plain = min(plain, to_adapt - 1);
+      for (int j = 0; j < plain; ++j) {
+        kkt();
+        if (p.check_termination) --to_check;
+        if (p.adaptive_rho) --to_adapt;
+        update(IC<0>{});
+        if (iter == 60) WV_MARK(46);
+        if (iter == 60) WV_MARK(47);
+        ++iter;
+      }
+    }
+#endif
+    const bool tm_it = iter == 60;
+    kkt();
+    bool is_check = false, is_adapt = false;
+    if (p.check_termination && --to_check == 0) {
+      is_check = true;
+      to_check = p.check_termination;
+    }
+    if (p.adaptive_rho && --to_adapt == 0) {
+      is_adapt = true;
+      to_adapt = p.adaptive_rho_interval;
+    }
+    const bool last = iter == p.max_iter;
+    const bool need_info = is_check || is_adapt || last;
+
     if (need_info) update(IC<1>{});
     else update(IC<0>{});
 

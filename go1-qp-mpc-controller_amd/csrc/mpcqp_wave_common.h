@@ -762,9 +762,11 @@ constexpr double SCHUR_GRAM_TOL = 1e-6;
 // max_i S_ii above which the Schur form hands a robot to the Riccati form (mpcqp_schur.h).
 // Measured (profiles/r04/smax, tools/fuzz_parity.py): four feet in contact, state weights x 5 /
 // x 100: u0 off the oracle by 4e-4 / 1e-3 without the hand-off, 9e-7 with it at 1e4; no C2 (trot)
-// robot crosses 1e4; a threshold of 1e3 sends most C2 robots to the Riccati form (-35 %)
+// robot crosses 1e4; a threshold of 1e3 sends most C2 robots to the Riccati form (-35 %).  Round 5
+// (profiles/r05/smax_r05): at 3e3 the mixed-gait fixtures' worst u0 error drops from 1.3e-7 to
+// 1.2e-11 (C5's sample: 3.9e-7 -> 2.7e-9) for 0.6 % of C5's time and none of C2's
 #ifndef MPCQP_SCHUR_SMAX
-#define MPCQP_SCHUR_SMAX 1e4
+#define MPCQP_SCHUR_SMAX 3e3
 #endif
 constexpr double SCHUR_SMAX = MPCQP_SCHUR_SMAX;
 template <int N>
