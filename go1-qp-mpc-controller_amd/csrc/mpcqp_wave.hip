@@ -814,15 +814,15 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
       Z4[r] = AK4[r] * xz;
     }
   }
-  auto rho4_of = [&](int r, double rho) __attribute__((always_inline)) {
-    const bool loose = L4[r] < -OSQP_INF * MIN_SCALING && U4[r] > OSQP_INF * MIN_SCALING;
-    const bool eq = U4[r] - L4[r] < RHO_TOL;
+  auto rho4_of = [&](double l4, double u4, double rho) __attribute__((always_inline)) {
+    const bool loose = l4 < -OSQP_INF * MIN_SCALING && u4 > OSQP_INF * MIN_SCALING;
+    const bool eq = u4 - l4 < RHO_TOL;
     return loose ? RHO_MIN : (eq ? RHO_EQ_OVER_RHO_INEQ * rho : rho);
   };
   double RI4[R];  // 1 / rho of row 4 (OSQP rho_inv_vec), refreshed with rho
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    RHO4[r] = rho4_of(r, rho0);
+    RHO4[r] = rho4_of(L4[r], U4[r], rho0);
     RI4[r] = 1. / RHO4[r];
   }
   if (mode != 0) {
@@ -832,6 +832,39 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
       const double at = quad_at(rho0 * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
       RHS[r] = vvr[r] ? (sigma * X[r] - Qv[r]) + at : 0.0;
     }
+  }
+  // Row 4 of every foot (the fz bounds row; its values are the same on the foot's four lanes) packed
+  // four register rounds to a register: lane a of a foot's quad holds round 4p + a's value in P[p].
+  // The ADMM update projects row 4 once per packed register instead of once per round, and the loop
+  // carries 7 NP doubles for it instead of 7 R (NP = 1 at N <= 12): fewer registers for the
+  // allocator to park in AGPRs.  unpack(P, r) is round r's value on all four lanes (a quad
+  // broadcast), bitwise the value the per-round arrays held.
+  constexpr int NP = (R + 3) / 4;
+  auto unpack = [&](const double (&P)[NP], int r) __attribute__((always_inline)) -> double {
+    const double v = P[r >> 2];
+    switch (r & 3) {
+      case 0: return dpp<QP_B0>(v);
+      case 1: return dpp<QP_B1>(v);
+      case 2: return dpp<QP_B2>(v);
+      default: return dpp<QP_B3>(v);
+    }
+  };
+  auto pack_of = [&](auto get, int pr) __attribute__((always_inline)) -> double {
+    const int r0 = 4 * pr, rl = R - 1;
+    const double v0 = get(r0 < rl ? r0 : rl), v1 = get(r0 + 1 < rl ? r0 + 1 : rl);
+    const double v2 = get(r0 + 2 < rl ? r0 + 2 : rl), v3 = get(r0 + 3 < rl ? r0 + 3 : rl);
+    return a == 0 ? v0 : (a == 1 ? v1 : (a == 2 ? v2 : v3));
+  };
+  double Z4P[NP], Y4P[NP], L4P[NP], U4P[NP], AK4P[NP], RHO4P[NP], RI4P[NP];
+#pragma unroll
+  for (int pr = 0; pr < NP; ++pr) {
+    Z4P[pr] = pack_of([&](int r) { return Z4[r]; }, pr);
+    Y4P[pr] = pack_of([&](int r) { return Y4[r]; }, pr);
+    L4P[pr] = pack_of([&](int r) { return L4[r]; }, pr);
+    U4P[pr] = pack_of([&](int r) { return U4[r]; }, pr);
+    AK4P[pr] = pack_of([&](int r) { return AK4[r]; }, pr);
+    RHO4P[pr] = pack_of([&](int r) { return RHO4[r]; }, pr);
+    RI4P[pr] = pack_of([&](int r) { return RI4[r]; }, pr);
   }
   if (KS == 0 && mode != 0) {
     // P~x of the warm iterate (the Riccati variant carries P~x through the KKT identity from here):
@@ -980,7 +1013,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
         // quotients: no reload of D, no division here)
         const double dir = DI[r];
         const double i0 = dpp<QP_B0>(dir), i1 = dpp<QP_B1>(dir), i2 = dpp<QP_B2>(dir);
-        const double ak4 = AK4[r], r4 = RHO4[r];
+        const double ak4 = unpack(AK4P, r), r4 = unpack(RHO4P, r);
         // rows of the foot: r0 [k00,0,k10] r1 [k01,0,k11] r2 [0,k02,k12] r3 [0,k03,k13] r4 [0,0,ak4]
         auto coef = [&](int row, int col) __attribute__((always_inline)) {
           if (row == 4) return col == 2 ? ak4 : 0.0;
@@ -1343,46 +1376,56 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
 
     // ---- update_x / update_z / update_y, and P~x by the KKT identity P~x~ = rhs - sigma x~ - A~'rho A~x~
     // this iteration's deltas, for the infeasibility tests of a need_info iteration only
-    double DX[R], DY[R], DY4[R], PXO[R];
+    double DX[R], DY[R], DY4P[NP], PXO[R];
     auto update = [&](auto INFO) __attribute__((always_inline)) {
       constexpr bool info = decltype(INFO)::value;
+      double xt[R], xz[R], zt[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const double xt = DI[r] * U[r];
-      const double xp = dpp<QP_PRIM>(xt), xz = dpp<QP_B2>(xt);
-      const double zt = AK0[r] * xp + AK1[r] * xz;
-      const double zt4 = AK4[r] * xz;
+      xt[r] = DI[r] * U[r];
+      const double xp = dpp<QP_PRIM>(xt[r]);
+      xz[r] = dpp<QP_B2>(xt[r]);
+      zt[r] = AK0[r] * xp + AK1[r] * xz[r];
       {  // (fmin/fmax = the reference's c_min/c_max on these non-NaN operands)
-        const double zr = alpha * zt + (1.0 - alpha) * Z[r];
+        const double zr = alpha * zt[r] + (1.0 - alpha) * Z[r];
         const double zn = fmin(fmax(zr + rinv * Y[r], LO03), HI03);
         const double dyv = rho * (zr - zn);
         Z[r] = zn;
         Y[r] = Y[r] + dyv;
         if constexpr (info) DY[r] = dyv;
       }
-      {
-        const double r4 = RHO4[r];
-        const double zr = alpha * zt4 + (1.0 - alpha) * Z4[r];
-        const double zn = fmin(fmax(zr + RI4[r] * Y4[r], L4[r]), U4[r]);
-        const double dyv = r4 * (zr - zn);
-        Z4[r] = zn;
-        Y4[r] = Y4[r] + dyv;
-        if constexpr (info) DY4[r] = dyv;
-      }
+    }
+      // row 4, packed: lane a projects round 4 pr + a
+      double V4P[NP], T4P[NP];
+#pragma unroll
+    for (int pr = 0; pr < NP; ++pr) {
+      const double zt4 = AK4P[pr] * pack_of([&](int r) { return xz[r]; }, pr);
+      const double r4 = RHO4P[pr];
+      const double zr = alpha * zt4 + (1.0 - alpha) * Z4P[pr];
+      const double zn = fmin(fmax(zr + RI4P[pr] * Y4P[pr], L4P[pr]), U4P[pr]);
+      const double dyv = r4 * (zr - zn);
+      Z4P[pr] = zn;
+      Y4P[pr] = Y4P[pr] + dyv;
+      if constexpr (info) DY4P[pr] = dyv;
+      V4P[pr] = RHO4P[pr] * Z4P[pr] - Y4P[pr];
+      T4P[pr] = KS == 0 ? RHO4P[pr] * zt4 : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
       // every lane updates (values of padding lanes / steps past N are never read unmasked)
       const double xo = X[r];
-      const double xn = alpha * xt + (1.0 - alpha) * xo;
+      const double xn = alpha * xt[r] + (1.0 - alpha) * xo;
       if constexpr (info) DX[r] = xn - xo;
       X[r] = xn;
+      const double ak4 = unpack(AK4P, r);
       if constexpr (KS == 0) {  // the Riccati variant carries P~x; the Schur form computes it at checks
-        const double kd = quad_at(rho * zt, RHO4[r] * zt4, AK0[r], AK1[r], AK4[r], a);
-        const double pxt = (RHS[r] - sigma * xt) - kd;
+        const double kd = quad_at(rho * zt[r], unpack(T4P, r), AK0[r], AK1[r], ak4, a);
+        const double pxt = (RHS[r] - sigma * xt[r]) - kd;
         if constexpr (info) PXO[r] = PX[r];
         PX[r] = alpha * pxt + (1.0 - alpha) * PX[r];
       }
-      // next right-hand side sigma x - q~ + A~'(rho z - y), here so that it interleaves with the other
-      // rounds' updates (recomputed below when adapt_rho changes rho)
-      const double at = quad_at(rho * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
+      // next right-hand side sigma x - q~ + A~'(rho z - y) (recomputed below when adapt_rho changes rho)
+      const double at = quad_at(rho * Z[r] - Y[r], unpack(V4P, r), AK0[r], AK1[r], ak4, a);
       RHS[r] = (sigma * X[r] - Qv[r]) + at;
     }
     };
@@ -1432,6 +1475,17 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
       // D and E of the lane's variables / rows.  The Riccati form loads them for the whole check in
       // one batch (one memory round trip instead of one per round: C4 +1.4 %); the Schur form where
       // they are used (holding them through P~x made its check slower: C2 -2 %, profiles/r05)
+      // row 4 per round (the packed registers unpacked for the check)
+      double Z4[R], Y4[R], L4[R], U4[R], AK4[R], DY4[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        Z4[r] = unpack(Z4P, r);
+        Y4[r] = unpack(Y4P, r);
+        L4[r] = unpack(L4P, r);
+        U4[r] = unpack(U4P, r);
+        AK4[r] = unpack(AK4P, r);
+        DY4[r] = unpack(DY4P, r);
+      }
       double DVc[R], EVc[R], E4c[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -1632,16 +1686,16 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
       }
       if (refactor) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          RHO4[r] = rho4_of(r, rho);
-          RI4[r] = 1. / RHO4[r];
+        for (int pr = 0; pr < NP; ++pr) {
+          RHO4P[pr] = rho4_of(L4P[pr], U4P[pr], rho);
+          RI4P[pr] = 1. / RHO4P[pr];
         }
         rinv = 1. / rho;
         need_factor = true;
         // the right-hand side with the new rho vector
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const double at = quad_at(rho * Z[r] - Y[r], RHO4[r] * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
+          const double at = quad_at(rho * Z[r] - Y[r], unpack(RHO4P, r) * Z4[r] - Y4[r], AK0[r], AK1[r], AK4[r], a);
           RHS[r] = (sigma * X[r] - Qv[r]) + at;
         }
       }
@@ -1678,12 +1732,13 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
         ws[WL::AK + m + ri] = AK1[r];
         ws[WL::Z + ri] = Z[r];
         ws[WL::Y + ri] = Y[r];
+        const double ak4 = unpack(AK4P, r), z4 = unpack(Z4P, r), y4 = unpack(Y4P, r);
         if (a == 0) {
           ws[WL::E + r4] = e4_of(r);
           ws[WL::AK + r4] = 0.0;
-          ws[WL::AK + m + r4] = AK4[r];
-          ws[WL::Z + r4] = Z4[r];
-          ws[WL::Y + r4] = Y4[r];
+          ws[WL::AK + m + r4] = ak4;
+          ws[WL::Z + r4] = z4;
+          ws[WL::Y + r4] = y4;
         }
       }
     }
