@@ -225,7 +225,8 @@ def main():
     if path is None:
         path = os.path.join(tempfile.mkdtemp(), "w.s")
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-strict-aliasing",
-                        f"-DMPCQP_WAVE_FOR_EACH_N(X)=X({a.n})", "--cuda-device-only", "-S", SRC, "-o", path] + a.defs,
+                        f"-DMPCQP_WAVE_FOR_EACH_N(X)=X({a.n})", "--cuda-device-only", "-S", SRC, "-o", path] + a.defs
+                       + os.environ.get("ISA_EXTRA_FLAGS", "").split(),
                        check=True, stderr=subprocess.DEVNULL)
     text = open(path).read()
     names = a.kernels or [f"wave_kernelILi{a.n}ELi1E", f"wave_kernelILi{a.n}ELi0E", f"scale_kernelILi{a.n}E"]
