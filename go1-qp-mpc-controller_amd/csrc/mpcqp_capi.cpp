@@ -31,6 +31,7 @@ struct mpcqp_handle {
   static constexpr int KMAX = 8;
   int split = 0;             // parts per solve: 0 = auto (split_parts), else MPCQP_SPLIT / mpcqp_set_split
   int fb_parts = 1;          // parts of the last solve (hand-off counters to sum)
+  int split_w[KMAX] = {};    // relative part sizes (MPCQP_SPLIT_W="w0,w1,..."); all 0 = equal parts
   hipStream_t sub[KMAX] = {};
   hipEvent_t ev_fork = nullptr;
   hipEvent_t ev_join[KMAX] = {};
@@ -279,6 +280,15 @@ int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** 
   h->slots = cus * per_cu;
   h->cus = cus;
   if (const char* sp = getenv("MPCQP_SPLIT")) h->split = atoi(sp);
+  if (const char* sw = getenv("MPCQP_SPLIT_W")) {
+    for (int i = 0; i < mpcqp_handle::KMAX && *sw; ++i) {
+      char* end = nullptr;
+      const long v = strtol(sw, &end, 10);
+      if (end == sw) break;
+      h->split_w[i] = v > 0 && v < 1000 ? (int)v : 0;
+      sw = *end == ',' ? end + 1 : end;
+    }
+  }
   e = ensure_split_streams(h);
   if (e != hipSuccess) { mpcqp_destroy(h); return MPCQP_ERR_HIP; }
   *out = h;
@@ -354,8 +364,19 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
       e = hipEventRecord(h->ev_fork, (hipStream_t)stream);
       const size_t rs = (size_t)MPCQP_REC_SIZE(h->p.horizon), n = (size_t)MPCQP_NUM_DOF * h->p.horizon;
       const size_t ws = (size_t)mpcqp::warm_state_doubles(h->p.horizon);
+      // part boundaries: equal parts, or relative sizes split_w when every part gets a robot
+      int bnd[mpcqp_handle::KMAX + 1];
+      int64_t wsum = 0;
+      for (int i = 0; i < parts; ++i) wsum = h->split_w[i] > 0 && wsum >= 0 ? wsum + h->split_w[i] : -1;
+      bool weighted = wsum > 0;
+      for (int i = 0, wc = 0; i <= parts; ++i) {
+        bnd[i] = (int)(weighted ? (int64_t)batch * wc / wsum : (int64_t)batch * i / parts);
+        if (i < parts && weighted) wc += h->split_w[i];
+      }
+      for (int i = 0; i < parts && weighted; ++i) weighted = bnd[i + 1] > bnd[i];
+      for (int i = 0; i <= parts && !weighted; ++i) bnd[i] = (int)((int64_t)batch * i / parts);
       for (int i = 0; i < parts && e == hipSuccess; ++i) {
-        const int b0 = (int)((int64_t)batch * i / parts), b1 = (int)((int64_t)batch * (i + 1) / parts);
+        const int b0 = bnd[i], b1 = bnd[i + 1];
         mpcqp::LaunchArgs ai = a;
         ai.recs = d_records + rs * b0;
         ai.batch = b1 - b0;
