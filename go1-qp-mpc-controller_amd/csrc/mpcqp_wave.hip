@@ -343,8 +343,32 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   // and rho); a changed pattern or mu -> re-init (fresh scaling and rho, the previous unscaled x, y)
   bool pattern_changed = false;
   SC_MARK(2);
+  // The raw norms only enter the bound-decided passes below, where an upper bound serves as well
+  // (their tests then err on the side of the exact passes): for nonnegative weights H is symmetric
+  // positive semidefinite, so max_i |H_ij| <= sqrt(H_jj max_i H_ii), from H's diagonal alone (one
+  // block of column j instead of N; the margin covers the roundings of the computed entries).  The
+  // first pass, which compares the raw norm itself with |A col j|, takes the bound only when the
+  // bound already loses that comparison in every column (checked below; else the exact norms).
+  bool cm_ub = true;
+#ifndef MPCQP_SCALE_EXACT_CM0
+  for (int i = 0; i < ND; ++i) cm_ub = cm_ub && p.q_weights[i] >= 0.0 && p.r_weights[i % MPCQP_NUM_DOF] >= 0.0;
+#else
+  cm_ub = false;
+#endif
+  auto colmax_ub = [&]() __attribute__((always_inline)) -> double {
+    double hd = 0.0;
+    if (lead && j0 < n) {
+      const int a2 = j0 % ND;
+      gen_col<N, 1, true>(sm, p, A, dtm, j0, j0 / ND, [&](int, int b, int, double hv) __attribute__((always_inline)) {
+        hd = b == a2 ? hv : hd;
+      });
+    }
+    double unused = 0.0, hm = hd;
+    block_sum_max<SC::NWS>(unused, hm, sm.red);
+    return sqrt(dmax(hd, 0.0) * hm) * (1.0 + 0x1p-20);
+  };
   if (p.scaling > 0 || ws) {
-    cm = colmax(true);
+    cm = cm_ub ? colmax_ub() : colmax(true);
     if (ws) pattern_changed = __syncthreads_or(pattern()) != 0;
   }
   // A is set once per solver init (A1RobotControl.cpp:526-530); a changed mu re-initializes
@@ -377,6 +401,27 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   // decided by the bounds, H's entries being far below A's unit entries.)
   if (lead && j0 < n) sm.cm0[j0] = cm;
   __syncthreads();
+  if (cm_ub && p.scaling > 0) {
+    // the first pass's fmax(c D_j cm_j, |A~ col j| D_j) with c = D_j = E_i = 1: the bound must lose it
+    // (then the raw norm, at most the bound, loses it too and the pass is the same)
+    bool wins = false;
+    if (t < 4 * N) {
+      const double* a0 = sm.Ap[0] + 5 * t;
+      const double* a1 = sm.Ap[1] + 5 * t;
+      const double* cz = sm.cm0 + 3 * t;
+      const double m0 = dmax(Ec[5 * t] * dabs(a0[0]), Ec[5 * t + 1] * dabs(a0[1]));
+      const double m1 = dmax(Ec[5 * t + 2] * dabs(a0[2]), Ec[5 * t + 3] * dabs(a0[3]));
+      const double m2 = dmax(dmax(dmax(dmax(dabs(a1[0]) * Ec[5 * t], dabs(a1[1]) * Ec[5 * t + 1]),
+                                       dabs(a1[2]) * Ec[5 * t + 2]), dabs(a1[3]) * Ec[5 * t + 3]),
+                             Ec[5 * t + 4] * dabs(a1[4]));
+      wins = !(cz[0] <= m0 * Dc[3 * t]) || !(cz[1] <= m1 * Dc[3 * t + 1]) || !(cz[2] <= m2 * Dc[3 * t + 2]);
+    }
+    if (__syncthreads_or(wins)) {
+      cm = colmax(true);
+      if (lead && j0 < n) sm.cm0[j0] = cm;
+      __syncthreads();
+    }
+  }
   int pass = 0;
   bool resume = false;  // the bound passes stopped after the D, E, q update of `pass`
   {
