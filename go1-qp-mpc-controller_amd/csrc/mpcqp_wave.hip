@@ -68,6 +68,9 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   const int inst = blockIdx.x;
   if (inst >= batch) return;
   const int t = threadIdx.x;
+#ifdef MPCQP_SCALE_TIMING
+  const double t_entry = (double)__builtin_readcyclecounter();
+#endif
   // wave_kernel's hand-off counters start at zero (stream order): [0] rank-deficient feet, [1]
   // (unused: an ill-conditioned core at the initial rho, never seen; see the flag below), [2] an
   // ill-conditioned Schur core after a rho update
@@ -83,6 +86,13 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
     if (__syncthreads_or(bad)) return;  // wave_kernel reports the non-finite record
   }
   SC_MARK(0);
+#ifdef MPCQP_SCALE_TIMING
+  if (t == 0) {  // kernel entry (before the record load), kept until the record's first words are read
+    double* tm_ = const_cast<double*>(recs) + (size_t)blockIdx.x * Cfg<N>::REC + 14;
+    tm_[0] = 7;
+    tm_[1] = t_entry;
+  }
+#endif
   const double* rec = sm.rec;
   const double dt = rec[MPCQP_REC_DT], mass = rec[MPCQP_REC_MASS], mu = rec[MPCQP_REC_MU];
   Adisc A;
@@ -149,7 +159,8 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
         }
         wave_sync();
       }
-    } else if (t < 64 + N) {
+      SC_MARK(8);
+    } else if (N <= 10 && t < 64 + N) {  // (the Schur form serves N <= 10 only: no screen beyond)
       // Degenerate-foot screen for the Schur form (wave_kernel KS = 1), by wave 1 while wave 0 runs
       // the sweep: per step k the Cholesky pivots of the Gram matrix B6_k B6_k' (B6 = rows 6-11 of
       // B_d(k): I_w^-1 [r_l]x dt and dt/m sums) relative to its diagonal.  Collinear feet give rank
