@@ -55,6 +55,16 @@ __device__ __forceinline__ int opaque(int v) {
 // Pins a value read from LDS into a register: the asm hides where it came from, so the compiler
 // cannot rematerialize it later by reloading LDS that has been reused in between.
 __device__ __forceinline__ void keep(double& v) { asm volatile("" : "+v"(v)); }
+// arr[i] for a per-lane i in [0, K): a select chain over the wave-uniform elements.  (Indexing the
+// kernel's by-value parameters with a per-lane index makes the compiler copy them to scratch memory
+// and load from there: a store and a load round trip through the memory pipe per robot.)
+template <int K>
+__device__ __forceinline__ double lane_pick(const double (&arr)[K], int i) {
+  double v = arr[0];
+#pragma unroll
+  for (int k = 1; k < K; ++k) v = i == k ? arr[k] : v;
+  return v;
+}
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 __device__ __forceinline__ double dabs(double a) { return __builtin_fabs(a); }

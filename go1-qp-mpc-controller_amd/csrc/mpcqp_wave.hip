@@ -911,16 +911,22 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
     const double v2 = get(r0 + 2 < rl ? r0 + 2 : rl), v3 = get(r0 + 3 < rl ? r0 + 3 : rl);
     return a == 0 ? v0 : (a == 1 ? v1 : (a == 2 ? v2 : v3));
   };
+  // (the setup's operands through a register copy: a select among loads of one local array is
+  // otherwise folded into one load at a per-lane address, which keeps the array in scratch memory)
+  auto reg = [](double v) __attribute__((always_inline)) {
+    asm("" : "+v"(v));
+    return v;
+  };
   double Z4P[NP], Y4P[NP], L4P[NP], U4P[NP], AK4P[NP], RHO4P[NP], RI4P[NP];
 #pragma unroll
   for (int pr = 0; pr < NP; ++pr) {
-    Z4P[pr] = pack_of([&](int r) { return Z4[r]; }, pr);
-    Y4P[pr] = pack_of([&](int r) { return Y4[r]; }, pr);
-    L4P[pr] = pack_of([&](int r) { return L4[r]; }, pr);
-    U4P[pr] = pack_of([&](int r) { return U4[r]; }, pr);
-    AK4P[pr] = pack_of([&](int r) { return AK4[r]; }, pr);
-    RHO4P[pr] = pack_of([&](int r) { return RHO4[r]; }, pr);
-    RI4P[pr] = pack_of([&](int r) { return RI4[r]; }, pr);
+    Z4P[pr] = pack_of([&](int r) { return reg(Z4[r]); }, pr);
+    Y4P[pr] = pack_of([&](int r) { return reg(Y4[r]); }, pr);
+    L4P[pr] = pack_of([&](int r) { return reg(L4[r]); }, pr);
+    U4P[pr] = pack_of([&](int r) { return reg(U4[r]); }, pr);
+    AK4P[pr] = pack_of([&](int r) { return reg(AK4[r]); }, pr);
+    RHO4P[pr] = pack_of([&](int r) { return reg(RHO4[r]); }, pr);
+    RI4P[pr] = pack_of([&](int r) { return reg(RI4[r]); }, pr);
   }
   if (KS == 0 && mode != 0) {
     // P~x of the warm iterate (the Riccati variant carries P~x through the KKT identity from here):
@@ -950,7 +956,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
         }
         const double xn = s + bu;
         HS.vec[(i + 1) & 1][t] = xn;
-        HS.lam[i][t] = 2 * p.q_weights[t] * xn;
+        HS.lam[i][t] = 2 * lane_pick(p.q_weights, t) * xn;
       }
       wave_sync();
     }
@@ -963,7 +969,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
       const int k = vvr[r] ? 4 * r + ig : 0;
       const double* lm = HS.lam[k];
       const double hv = (((sm.Bw[k][0][idx] * lm[6] + sm.Bw[k][1][idx] * lm[7]) + sm.Bw[k][2][idx] * lm[8]) +
-                         dtm * lm[9 + idx % 3]) + (2 * p.r_weights[idx]) * HS.Dt[ND * k + idx];
+                         dtm * lm[9 + idx % 3]) + (2 * lane_pick(p.r_weights, idx)) * HS.Dt[ND * k + idx];
       PX[r] = vvr[r] ? (c_s * Dv[r]) * hv : 0.0;
     }
   }
@@ -1003,13 +1009,14 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
 
   // ---- 5. ADMM (osqp_solve) ------------------------------------------------------------------------
   auto& F = sm.u.f;
-  // per-lane weights, loaded once (a per-lane index into the kernel parameters is a memory round
-  // trip): 2 r of the lane's variable component, 2 q_(6+c) of its impulse component (KS = 1)
-  double R2I = 2.0 * p.r_weights[idx], Q2C = 2.0 * p.q_weights[6 + (t < 6 * N ? t : 0) % 6];
+  // per-lane weights, selected once (lane_pick: a per-lane index into the kernel parameters is a
+  // scratch copy and a memory round trip): 2 r of the lane's variable component, 2 q_(6+c) of its
+  // impulse component (KS = 1)
+  double R2I = 2.0 * lane_pick(p.r_weights, idx), Q2C = 2.0 * lane_pick(p.q_weights, 6 + (t < 6 * N ? t : 0) % 6);
   keep(R2I);
   keep(Q2C);
   // KS = 0: 2 q_j of the MFMA column j = lane & 15 (factorize_mfma's cQ diagonal)
-  double Q2J = KS == 0 ? 2.0 * p.q_weights[li < ND ? li : 0] : 0.0;
+  double Q2J = KS == 0 ? 2.0 * lane_pick(p.q_weights, li < ND ? li : 0) : 0.0;
   keep(Q2J);
   // KS = 0 without stored Acl: the lane's coefficients of A' on states 0-5 (lane of state i: A[s][i])
   // and of A on states 6-11 (A[i][6 + s]), the off-diagonal part of the discrete A
