@@ -798,12 +798,14 @@ struct ScaleCfg {
   // wave 0 runs the gradient sweep, so N <= 5 (n <= 60) still launches threads 64 .. 64 + N - 1
   static constexpr int NTS = ((TPC * n + 63) / 64) * 64 > 64 + N ? ((TPC * n + 63) / 64) * 64 : ((64 + N + 63) / 64) * 64;
   static constexpr int NWS = NTS / 64;
-  // waves per SIMD the register allocation must allow (launch bounds): N = 10, two waves per robot,
-  // four robots per CU; N = 20, four waves per robot, three per CU (measured, profiles/r04/occ)
+  // waves per SIMD the register allocation must allow (launch bounds): two, i.e. 256 VGPRs and no
+  // spills.  N = 10: two waves per robot, four robots per CU; N = 20: four waves per robot, two per
+  // CU (three per CU spilled 43 VGPRs: the same step time, 21 MB more HBM traffic per C4 solve,
+  // profiles/r05/w20; three waves at N = 10 is slower, profiles/r05/sweep_reg)
 #ifdef MPCQP_SCALE_WPE
   static constexpr int WPE = MPCQP_SCALE_WPE;
 #else
-  static constexpr int WPE = N <= 10 ? 2 : 3;
+  static constexpr int WPE = 2;
 #endif
   static constexpr int RPT = (m + NTS - 1) / NTS;   // constraint rows per thread
 };
