@@ -79,6 +79,34 @@ def load_traffic(config_key, kernel):
     return e.get("hbm_bytes_per_launch")
 
 
+def load_executed(config_key, kernel):
+    """Executed binary64 FLOPs per solve of `kernel` from a separate rocprofv3 --pmc pass
+    (profiles/pmc_flops.json, tools/pmc_flops.py: SQ_INSTS_VALU_{FMA,ADD,MUL}_F64 x 64 lanes, FMA = 2,
+    plus SQ_INSTS_VALU_MFMA_MOPS_F64 x 512), or None when no pass of that kernel is on file.  An upper
+    bound on useful FLOPs: masked and padding lanes are counted."""
+    path = os.path.join(REPO, "profiles", "pmc_flops.json")
+    try:
+        with open(path) as f:
+            e = json.load(f).get(config_key, {})
+    except (OSError, ValueError):
+        return None
+    names = " + ".join(k.get("kernel", "") for k in e.get("kernels", [])).replace(" ", "")
+    for part in kernel.split(" + "):
+        short = part.split("::")[-1].split("<")[0]
+        tmpl = part[part.find("<"):part.find(">") + 1] if "<" in part else ""
+        if (short + tmpl).replace(" ", "") not in names:
+            return None
+    return e.get("executed_f64_flop_per_solve")
+
+
+def executed_fields(config_key, kernel, ms):
+    ex = load_executed(config_key, kernel)
+    if ex is None:
+        return {"executed_flop_per_launch": None, "executed_tflops": None, "executed_frac": None}
+    tf = ex / (ms * 1e-3) / 1e12
+    return {"executed_flop_per_launch": ex, "executed_tflops": tf, "executed_frac": tf / FP64_PEAK_TFLOPS}
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -320,6 +348,9 @@ def run_rank(args):
                 "bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS, "traffic": load_traffic(key, eff_name),
                 "kernel": eff_name, "kernel_ms": kern_ms, "algorithmic_flop_per_launch": flops,
+                # the FLOPs the kernels actually issue (PMC pass, profiles/pmc_flops.json) over the same
+                # span: the Schur form executes fewer than SURVEY §8(d)'s dense count
+                **executed_fields(key, eff_name, kern_ms),
                 "parts": solver.split_parts(Bl),
                 "kernel_ms_what": ("span of one solve call on the caller's stream (HIP events): the batch's "
                                    "scale_kernel + wave_kernel pairs, split into `parts` concurrent parts on the "
@@ -575,6 +606,7 @@ def extras(args, solver, params, recs_np, states, base_res, pyoracle, dev):
     ent = {"value": B4 / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms, "batch": B4, "horizon": 20,
            "workload": "C4: horizon 20 (n=240, m=400), trot", "mean_iters": float(g4["iters"].mean()),
            "roofline_frac": fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+           **executed_fields("N20_B4096_trot", "mpcqp::wv::scale_kernel<20> + mpcqp::wv::wave_kernel<20, 0>", ms),
            # HBM bytes per launch of the N = 20 solve from its own rocprofv3 PMC pass (profiles/)
            "traffic": load_traffic("N20_B4096_trot",
                                    "mpcqp::wv::scale_kernel<20> + mpcqp::wv::wave_kernel<20, 0>"),

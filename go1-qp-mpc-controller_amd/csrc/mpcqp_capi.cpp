@@ -32,6 +32,8 @@ struct mpcqp_handle {
   int split = 0;             // parts per solve: 0 = auto (split_parts), else MPCQP_SPLIT / mpcqp_set_split
   int fb_parts = 1;          // parts of the last solve (hand-off counters to sum)
   int split_w[KMAX] = {};    // relative part sizes (MPCQP_SPLIT_W="w0,w1,..."); all 0 = equal parts
+  // sub[i] / ev_join[i] serve part i >= 1 (part 0 runs on the caller's stream), created lazily: only
+  // the parts - 1 streams a split of that size uses, the first time it runs or at mpcqp_reserve
   hipStream_t sub[KMAX] = {};
   hipEvent_t ev_fork = nullptr;
   hipEvent_t ev_join[KMAX] = {};
@@ -144,11 +146,16 @@ int split_parts(const mpcqp_handle* h, int32_t batch) {
   return k < 1 ? 1 : k;
 }
 
-// The internal streams and events of the batch split, created once per handle.
-hipError_t ensure_split_streams(mpcqp_handle* h) {
+// The internal streams and events of a split into `parts` parts: parts 1 .. parts-1 each get a stream
+// and a join event the first time a split of that size runs (or at mpcqp_reserve, for callers that
+// capture the solve into a graph).  Nothing is created for an unsplit solve, so a process's hardware
+// queues (GPU_MAX_HW_QUEUES = 4) are not filled with streams it never uses: a C3 rank holds the
+// caller's stream, RCCL's and the split's two.
+hipError_t ensure_split_streams(mpcqp_handle* h, int parts) {
   hipError_t e = hipSuccess;
+  if (parts < 2) return e;
   if (!h->ev_fork) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
-  for (int i = 0; i < mpcqp_handle::KMAX && e == hipSuccess; ++i) {
+  for (int i = 1; i < parts && i < mpcqp_handle::KMAX && e == hipSuccess; ++i) {
     if (!h->sub[i]) e = hipStreamCreateWithFlags(&h->sub[i], hipStreamNonBlocking);
     if (e == hipSuccess && !h->ev_join[i]) e = hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming);
   }
@@ -289,8 +296,6 @@ int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** 
       sw = *end == ',' ? end + 1 : end;
     }
   }
-  e = ensure_split_streams(h);
-  if (e != hipSuccess) { mpcqp_destroy(h); return MPCQP_ERR_HIP; }
   *out = h;
   return MPCQP_OK;
 }
@@ -359,9 +364,10 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
         break;
       }
       // fork: part 0 runs on the caller's stream, every other part on an internal stream that waits
-      // for the work queued on the caller's stream so far (parts + 0 streams more: a process has
+      // for the work queued on the caller's stream so far (parts - 1 streams more: a process has
       // few hardware queues, GPU_MAX_HW_QUEUES = 4, and streams beyond them share one in order)
-      e = hipEventRecord(h->ev_fork, (hipStream_t)stream);
+      e = ensure_split_streams(h, parts);
+      if (e == hipSuccess) e = hipEventRecord(h->ev_fork, (hipStream_t)stream);
       const size_t rs = (size_t)MPCQP_REC_SIZE(h->p.horizon), n = (size_t)MPCQP_NUM_DOF * h->p.horizon;
       const size_t ws = (size_t)mpcqp::warm_state_doubles(h->p.horizon);
       // part boundaries: equal parts, or relative sizes split_w when every part gets a robot
@@ -644,6 +650,8 @@ int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {
     e = hipDeviceSynchronize();
   if (e == hipSuccess) e = ensure_workspace(h, batch, nullptr);
   if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
+  if (effective_path(h) == 3) e = ensure_split_streams(h, split_parts(h, batch));
+  if (e != hipSuccess) return set_hip_error(h, e, "split streams");
   return MPCQP_OK;
 }
 int32_t mpcqp_solve_threads(int32_t horizon) {

@@ -641,6 +641,10 @@ __device__ __forceinline__ void schur_px(const SM& sm, SchurLds<N>& F, const mpc
   {
     double zc[4];
     rowbcast4(z, zc[0], zc[1], zc[2], zc[3]);
+    // all four row copies exist before the first block (which waits for them): otherwise the compiler
+    // may sink a copy's permlane to just before the first block that reads it, which has no wait
+    // (tools/isa_hazards.py --all found that at N = 7 and 8: a px_one block reading zc[1] / zc[2])
+    asm("" : "+&v"(zc[0]), "+&v"(zc[1]), "+&v"(zc[2]), "+&v"(zc[3]));
     double s1[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, s2[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     // alpha_kl = sum_{i >= max(k,l)} (i-k)(i-l): l >= k: (l-k) T1(N-1-l) + T2(N-1-l); l < k:
     // (k-l) T1(N-1-k) + T2(N-1-k), T1(m) = m(m+1)/2, T2(m) = m(m+1)(2m+1)/6 (all exact integers)

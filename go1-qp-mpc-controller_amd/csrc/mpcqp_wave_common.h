@@ -758,7 +758,10 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
 // form as before (see gen_col), so every norm is binary64; only the order of the cost-scaling sum
 // over columns differs from the single-wave version (a different but equally exact summation).
 // B6_k Gram pivot ratio below which a robot is handed to the Riccati form (scale_kernel's screen)
-constexpr double SCHUR_GRAM_TOL = 1e-6;
+#ifndef MPCQP_SCHUR_GRAM_TOL
+#define MPCQP_SCHUR_GRAM_TOL 1e-6
+#endif
+constexpr double SCHUR_GRAM_TOL = MPCQP_SCHUR_GRAM_TOL;
 // max_i S_ii above which the Schur form hands a robot to the Riccati form (mpcqp_schur.h).
 // Measured (profiles/r04/smax, tools/fuzz_parity.py): four feet in contact, state weights x 5 /
 // x 100: u0 off the oracle by 4e-4 / 1e-3 without the hand-off, 9e-7 with it at 1e4; no C2 (trot)

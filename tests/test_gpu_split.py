@@ -70,3 +70,49 @@ def test_split_warm_ticks_bitwise():
             outs[parts].append(state.cpu().numpy().view(np.uint64).copy())
     for a, b in zip(outs[1], outs[4]):
         assert np.array_equal(a, b)
+
+
+def _solve_full(s, recs, parts, trace_cap):
+    """Results, full-horizon solutions and check traces (the per-part offsets of the
+    solution and trace pointers, and trace_cap - b0, at every part boundary)."""
+    B = recs.shape[0]
+    s.set_split(parts)
+    d_rec = torch.from_numpy(recs).cuda()
+    res = torch.zeros((B, RD), dtype=torch.float64, device="cuda")
+    sol = torch.full((B, s.n), float("nan"), dtype=torch.float64, device="cuda")
+    tr = torch.full((B, 64, 4), -1.0, dtype=torch.float64, device="cuda")
+    s.solve_device_trace(d_rec.data_ptr(), B, res.data_ptr(), sol.data_ptr(), tr.data_ptr(), trace_cap,
+                         torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return [x.cpu().numpy().view(np.uint64).copy() for x in (res, sol, tr)]
+
+
+def test_split_solution_and_trace_offsets():
+    batch, trace_cap = 3001, 1700  # the cap ends inside part 1 of 3, inside part 3 of 7
+    st = mpcqp.synthetic_go1(batch, seed=78, gait="mixed", mixed_mu=True)
+    recs = mpcqp.assemble_compute_grf(st, 10)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+        s.reserve(batch)
+        ref = _solve_full(s, recs, 1, trace_cap)
+        for parts in (3, 7):
+            got = _solve_full(s, recs, parts, trace_cap)
+            for a, b, what in zip(got, ref, ("results", "solution", "trace")):
+                assert np.array_equal(a, b), f"parts={parts}: {what}"
+    # robots past the cap keep the untouched trace (-1.0)
+    assert np.all(ref[2].reshape(batch, -1)[trace_cap:] == np.float64(-1.0).view(np.uint64))
+    assert not np.any(np.isnan(ref[1].view(np.float64)))
+
+
+def test_weighted_split_bitwise(monkeypatch):
+    """MPCQP_SPLIT_W (read at handle creation) sizes the parts unevenly: part 0 a quarter, part 1
+    three quarters of the batch."""
+    batch = 4096
+    st = mpcqp.synthetic_go1(batch, seed=79, gait="trot")
+    recs = mpcqp.assemble_compute_grf(st, 10)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+        ref = _solve_full(s, recs, 1, batch)
+    monkeypatch.setenv("MPCQP_SPLIT_W", "1,3")
+    with mpcqp.MpcQpSolver(mpcqp.default_params(10)) as s:
+        got = _solve_full(s, recs, 2, batch)
+    for a, b, what in zip(got, ref, ("results", "solution", "trace")):
+        assert np.array_equal(a, b), what

@@ -217,6 +217,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--asm", default=None, help="assembly file (default: compile csrc/mpcqp_wave.hip)")
     ap.add_argument("--n", type=int, default=10)
+    ap.add_argument("--all", action="store_true",
+                    help="the product build's every horizon (N = 1..20: wave_kernel<N, 1> for N <= 10, "
+                         "wave_kernel<N, 0> and scale_kernel<N> for all) from one compile")
     ap.add_argument("--defs", nargs="*", default=[])
     ap.add_argument("--kernels", nargs="*", default=None)
     ap.add_argument("--max-report", type=int, default=40)
@@ -224,14 +227,23 @@ def main():
     path = a.asm
     if path is None:
         path = os.path.join(tempfile.mkdtemp(), "w.s")
-        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-strict-aliasing",
-                        f"-DMPCQP_WAVE_FOR_EACH_N(X)=X({a.n})", "--cuda-device-only", "-S", SRC, "-o", path] + a.defs
+        nflag = [] if a.all else [f"-DMPCQP_WAVE_FOR_EACH_N(X)=X({a.n})"]
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-strict-aliasing"]
+                       + nflag + ["--cuda-device-only", "-S", SRC, "-o", path] + a.defs
                        + os.environ.get("ISA_EXTRA_FLAGS", "").split(),
                        check=True, stderr=subprocess.DEVNULL)
     text = open(path).read()
-    names = a.kernels or [f"wave_kernelILi{a.n}ELi1E", f"wave_kernelILi{a.n}ELi0E", f"scale_kernelILi{a.n}E"]
+    if a.kernels:
+        names = a.kernels
+    elif a.all:
+        names = [f"wave_kernelILi{n}ELi1E" for n in range(1, 11)] + [f"wave_kernelILi{n}ELi0E" for n in range(1, 21)] \
+            + [f"scale_kernelILi{n}E" for n in range(1, 21)]
+    else:
+        names = [f"wave_kernelILi{a.n}ELi1E", f"wave_kernelILi{a.n}ELi0E", f"scale_kernelILi{a.n}E"]
     total = 0
+    seen = 0
     for nm, lines, l0 in kernels(text, names):
+        seen += 1
         probs, nins = check(lines, l0)
         kinds = {}
         for kd, _, _ in probs:
@@ -240,6 +252,9 @@ def main():
         for kd, ln, msg in probs[:a.max_report]:
             print(f"  [{kd}] line {ln}: {msg}")
         total += len(probs)
+    if seen < len(names):
+        print(f"only {seen} of the {len(names)} kernels found in the assembly")
+        return 1
     return 1 if total else 0
 
 
