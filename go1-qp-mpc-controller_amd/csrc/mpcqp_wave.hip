@@ -1857,8 +1857,17 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
   return false;
 }
 
+// waves per SIMD the register allocation must allow (experiment builds: MPCQP_WAVE_WPE=2 asks the
+// allocator for 256 registers, the budget of two robots per SIMD; profiles/r06/two_per_simd)
+#if defined(MPCQP_WAVE_NUM_VGPR)
+#define MPCQP_WAVE_BOUNDS __launch_bounds__(NT) __attribute__((amdgpu_num_vgpr(MPCQP_WAVE_NUM_VGPR)))
+#elif defined(MPCQP_WAVE_WPE)
+#define MPCQP_WAVE_BOUNDS __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MPCQP_WAVE_WPE)))
+#else
+#define MPCQP_WAVE_BOUNDS __launch_bounds__(NT, 1)
+#endif
 template <int N, int KS>
-__global__ __launch_bounds__(NT, 1) void wave_kernel(const double* __restrict__ recs, int batch,
+__global__ MPCQP_WAVE_BOUNDS void wave_kernel(const double* __restrict__ recs, int batch,
                                                      mpcqp_result* __restrict__ results,
                                                      double* __restrict__ solution, double* __restrict__ trace,
                                                      int trace_cap, double* __restrict__ wstate,

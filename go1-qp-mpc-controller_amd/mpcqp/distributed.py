@@ -53,6 +53,56 @@ def allgather_forces(local, total, group=None):
     return torch.cat(rows, 0)
 
 
+class ForceGather:
+    """Double-buffered asynchronous all-gather of the solved forces (the per-tick exchange of C3).
+
+    ``gather(results)`` copies u0 (the first ``k`` columns of the rank's result rows) into a send
+    buffer on the current stream and issues ``all_gather_into_tensor(async_op=True)``: the collective
+    runs on the backend's own stream (RCCL) beside the next tick's solve, which writes the results
+    again without waiting for it; a send / receive buffer pair is reused only after the collective
+    that last used it has completed (``Work.wait``: a stream dependency for RCCL, a host wait for gloo).
+    ``result(h)`` waits for gather ``h`` and returns the [total, k] forces (padding stripped);
+    ``drain()`` waits for every gather in flight.  Shards may differ by one row (balanced split):
+    the send buffer holds ceil(total / world) rows, as in ``allgather_forces``."""
+
+    def __init__(self, total, k=12, device=None, dtype=torch.float64, group=None, depth=2):
+        self.world = dist.get_world_size(group)
+        self.total, self.k, self.group = total, k, group
+        self.chunk = -(-total // self.world)
+        self.send = [torch.zeros((self.chunk, k), dtype=dtype, device=device) for _ in range(depth)]
+        self.out = [torch.empty((self.world * self.chunk, k), dtype=dtype, device=device) for _ in range(depth)]
+        self.works = [None] * depth
+        self.n = 0
+
+    def _wait(self, i):
+        if self.works[i] is not None:
+            self.works[i].wait()
+            self.works[i] = None
+
+    def gather(self, results):
+        i = self.n % len(self.send)
+        self._wait(i)
+        self.send[i][: results.shape[0]].copy_(results[:, : self.k])
+        self.works[i] = dist.all_gather_into_tensor(self.out[i], self.send[i], group=self.group, async_op=True)
+        self.n += 1
+        return i
+
+    def result(self, h):
+        self._wait(h)
+        out = self.out[h]
+        if self.chunk * self.world == self.total:
+            return out
+        rows = []
+        for r in range(self.world):
+            b, e = shard_range(self.total, self.world, r)
+            rows.append(out[r * self.chunk: r * self.chunk + (e - b)])
+        return torch.cat(rows, 0)
+
+    def drain(self):
+        for i in range(len(self.works)):
+            self._wait(i)
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

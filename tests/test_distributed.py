@@ -102,3 +102,35 @@ def test_bench_default_batch_is_c2_at_one_gpu_and_c3_shard_above():
     assert bench.config_name(10, 4096, 1, "trot", False) == "C2"
     assert bench.config_name(10, 8192, 8, "trot", False) == "C3"
     assert bench.config_name(20, 4096, 1, "trot", False) == "C4"
+
+
+def _fg_worker(rank, world, port, total, steps, out_dir):
+    from mpcqp.distributed import ForceGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, e = shard_range(total, world, rank)
+    fg = ForceGather(total, 12)
+    res = torch.zeros((e - b, 30), dtype=torch.float64)
+    hs = []
+    for t in range(steps):
+        # step t's "results": rows of 30 doubles whose first 12 identify (tick, robot, column)
+        res.copy_(torch.arange(b, e, dtype=torch.float64)[:, None] * 100.0 + torch.arange(30.0)[None, :] + 1e5 * t)
+        hs.append(fg.gather(res))
+        if t >= 1:  # the previous tick's forces are complete although this tick's gather is in flight
+            np.save(os.path.join(out_dir, f"r{rank}_t{t - 1}.npy"), fg.result(hs[t - 1]).numpy())
+    np.save(os.path.join(out_dir, f"r{rank}_t{steps - 1}.npy"), fg.result(hs[-1]).numpy())
+    fg.drain()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total", [10, 9])
+def test_force_gather_double_buffered(tmp_path, total):
+    """mpcqp.distributed.ForceGather (bench.py's per-tick exchange): every tick's gathered forces are
+    that tick's u0 of every rank, with the buffers reused every second tick and unequal shards."""
+    world, steps = 2, 5
+    mp.spawn(_fg_worker, args=(world, _free_port(), total, steps, str(tmp_path)), nprocs=world, join=True)
+    for t in range(steps):
+        exp = (np.arange(total, dtype=np.float64)[:, None] * 100.0 + np.arange(12.0)[None, :] + 1e5 * t)
+        for r in range(world):
+            np.testing.assert_array_equal(np.load(tmp_path / f"r{r}_t{t}.npy"), exp)

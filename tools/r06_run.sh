@@ -39,8 +39,10 @@ print("value", round(d["value"]), "ms", round(d["ms_per_step"], 4), "frac", roun
 for k, v in (d.get("extras") or {}).items():
     if isinstance(v, dict) and "value" in v:
         print(" ", k, round(v["value"]))
+def last(fn):
+    return json.loads([l for l in open(fn) if l.startswith("{")][-1])
 for sp in (0, 1):
-    a = json.load(open(f"{o}/dist_split{sp}.json")); b = json.load(open(f"{o}/plain_split{sp}.json"))
+    a = last(f"{o}/dist_split{sp}.json"); b = last(f"{o}/plain_split{sp}.json")
     print(f"split={sp} (0 = auto): dist {a['value']:.0f} plain {b['value']:.0f} ratio {a['value'] / b['value']:.3f} allgather_ms {a['extras']['allgather_ms']}")
 for r in csv.DictReader(open(o + "/trace/run_kernel_stats.csv")):
     print(r["Name"][:60], r["Calls"], r["AverageNs"])
