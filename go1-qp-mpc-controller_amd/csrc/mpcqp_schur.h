@@ -195,7 +195,8 @@ __device__ __forceinline__ double alpha_jl(int N, int j, int l) {
 // (G_k is positive definite for the robots that reach it: scale_kernel screens out rank-deficient
 // B6_k, whose robots the Riccati form solves)
 // smax: max_i S_ii (>= 1; a lower bound on the condition of S, whose eigenvalues are >= 1), from the
-// lanes' own V, W rows: S_ii = 1 + beta_kk |v_i|^2 + alpha_kk |w_i|^2.
+// lanes' own V, W rows: S_ii = 1 + beta_kk |v_i|^2 + alpha_kk |w_i|^2 (the hand-off at the checks
+// weighs it with the KKT solve's observed cancellation, schur_solve's amp).
 template <int N, int R, class SM, class Mark>
 __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp_params& p, const Adisc& A, double cost_c,
                              double dtm, double (&RI)[R][3], Mark&& mark, double& smax) {
@@ -366,7 +367,7 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
       sw += vw[6 + e] * vw[6 + e];
     }
     const double sii = (1.0 + (double)(N - k) * sv) + alpha_jl(N, k, k) * sw;
-    smax = __any(iv && !(sii <= SCHUR_SMAX)) ? 2.0 * SCHUR_SMAX : 1.0;
+    smax = wave_max(iv ? sii : 0.0);
   }
   mark(13);
   // S - I = L'CL = beta o (V V') + alpha o (W W') (V, W: the 6-column halves of vw; beta, alpha per
@@ -471,9 +472,12 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
 
 // ---- KKT solve (every ADMM iteration) ------------------------------------------------------------
 // W[r]: w = D^-1 rhs in the variable layout; returns U[r] = (c B6'M B6 + R')^-1 w.
-template <int N, int R>
+// AMP (update_info iterations): amp = max|R'^-1 w| / max|u| over the robot's variables, the
+// cancellation of the push-through identity u = R'^-1 w - B'(I - S^-1)B w in this solve: the rounding
+// errors of both terms (and of S^-1) reach u amplified by it.
+template <int N, int R, bool AMP = false>
 __device__ __forceinline__ void schur_solve(SchurLds<N>& F, const double (&W)[R], const double (&RI)[R][3],
-                                            const bool (&vvr)[R], double (&U)[R]) {
+                                            const bool (&vvr)[R], double (&U)[R], double& amp) {
   constexpr int NI = SchurCfg<N>::NI, QS = SchurCfg<N>::QS, BS = SchurCfg<N>::BS;
   const int t = threadIdx.x, q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
   const bool av = a < 3;
@@ -558,6 +562,17 @@ __device__ __forceinline__ void schur_solve(SchurLds<N>& F, const double (&W)[R]
     const double y = ((((bc[0] * qa.x + bc[BS] * qa.y) + bc[2 * BS] * qb.x) + bc[3 * BS] * qb.y) + bc[4 * BS] * qc.x) +
                      bc[5 * BS] * qc.y;
     U[r] = r1[r] - y;
+  }
+  if constexpr (AMP) {
+    double mr = 0.0, mu = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      mr = vvr[r] ? fmax(mr, dabs(r1[r])) : mr;
+      mu = vvr[r] ? fmax(mu, dabs(U[r])) : mu;
+    }
+    mr = wave_max(mr);
+    mu = wave_max(mu);
+    amp = mu > 0.0 ? mr / mu : (mr > 0.0 ? INFINITY : 1.0);
   }
 }
 

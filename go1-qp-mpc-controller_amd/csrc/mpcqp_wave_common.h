@@ -762,16 +762,26 @@ __device__ void factorize_mfma(SM& sm, const mpcqp_params& p, const Adisc& A, do
 #define MPCQP_SCHUR_GRAM_TOL 1e-6
 #endif
 constexpr double SCHUR_GRAM_TOL = MPCQP_SCHUR_GRAM_TOL;
-// max_i S_ii above which the Schur form hands a robot to the Riccati form (mpcqp_schur.h).
-// Measured (profiles/r04/smax, tools/fuzz_parity.py): four feet in contact, state weights x 5 /
-// x 100: u0 off the oracle by 4e-4 / 1e-3 without the hand-off, 9e-7 with it at 1e4; no C2 (trot)
-// robot crosses 1e4; a threshold of 1e3 sends most C2 robots to the Riccati form (-35 %).  Round 5
-// (profiles/r05/smax_r05): at 3e3 the mixed-gait fixtures' worst u0 error drops from 1.3e-7 to
-// 1.2e-11 (C5's sample: 3.9e-7 -> 2.7e-9) for 0.6 % of C5's time and none of C2's
+// The Schur form's hand-off to the Riccati form (mpcqp_schur.h), decided at every update_info
+// iteration from the latest factorization's max_i S_ii (a lower bound on the condition of S) and that
+// iteration's observed cancellation of the push-through identity, schur_solve's
+// amp = max|R'^-1 w| / max|u|: one KKT solve then loses about eps * S_max * amp of relative accuracy.
+// A robot leaves when S_max * amp > SCHUR_AMP or S_max > SCHUR_SMAX (a hard cap).
+// History: round 4 handed over on S_max > 1e4 (four feet in contact, state weights x 5 / x 100: u0 off
+// the oracle by 4e-4 / 1e-3 without a hand-off, 9e-7 with it); round 5 lowered that to 3e3 after a
+// loop change moved FMA contraction and the mixed-gait golden set from 1.0e-9 to 1.3e-7.  Round 6
+// (profiles/r06/cancel: 7,254 robots — stance / mixed at weights x 1, 5, 100, the golden sets, C2 and
+// C5 samples — solved to the end by the Schur form in builds with -ffp-contract=fast and =on): the
+// worst u0 error of the robots a bound keeps, S_max <= 3e3: 8.3e-9 (fast) / 6.8e-9 (on), 52 handed
+// over; S_max * amp <= 3e4: 1.1e-9 / 8.1e-10, 96 handed over (C2: 1 of 2048, C5: 24 of 2048).
 #ifndef MPCQP_SCHUR_SMAX
-#define MPCQP_SCHUR_SMAX 3e3
+#define MPCQP_SCHUR_SMAX 1e4
 #endif
 constexpr double SCHUR_SMAX = MPCQP_SCHUR_SMAX;
+#ifndef MPCQP_SCHUR_AMP
+#define MPCQP_SCHUR_AMP 3e4
+#endif
+constexpr double SCHUR_AMP = MPCQP_SCHUR_AMP;
 template <int N>
 struct ScaleImg {
   static constexpr int n = ND * N, m = CD * N;

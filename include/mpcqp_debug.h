@@ -42,6 +42,14 @@ int32_t mpcqp_debug_set_split(mpcqp_handle* h, int32_t parts);
 /* Parts a solve of `batch` robots on this handle is split into under its current setting. */
 int32_t mpcqp_debug_split_parts(mpcqp_handle* h, int32_t batch);
 
+/* Two-phase cold solve of the Schur form (horizons <= 10): robots still running after the update_info
+ * iteration `cut` park their state, are sorted by how far their dual residual is from its tolerance,
+ * and a second launch resumes them longest-first (a batch solved this way is one launch; results are
+ * bitwise those of the one-phase solve).  0 = one-phase; `cut` should be a multiple of
+ * check_termination; -1 only queries.  The environment variable MPCQP_PARK sets the initial value at
+ * mpcqp_create.  Returns the previous setting, or -MPCQP_ERR_INVALID_ARG. */
+int32_t mpcqp_debug_set_park(mpcqp_handle* h, int32_t cut);
+
 /* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */
 int32_t mpcqp_solve_threads(int32_t horizon);
 

@@ -3,7 +3,8 @@ wait only where the compiled code needs it (mpcqp_wave_common.h, DPP wait states
 must show no DPP / permlane / transcendental / untracked-load hazard.  Every horizon the product
 library instantiates is checked (each N is scheduled separately; the round-6 check found
 two real DPP hazards at N = 7 and 8 that the N = 10 / 20 check could not see): wave_kernel<N, 1> for
-N <= 10, wave_kernel<N, 0> and scale_kernel<N> for N = 1..20.  CPU only (hipcc -S, one compile per
+N <= 10 (one-phase, parking and resuming instantiations), wave_kernel<N, 0> and scale_kernel<N> for
+N = 1..20.  CPU only (hipcc -S, one compile per
 horizon, in parallel)."""
 import os
 import subprocess
@@ -13,8 +14,15 @@ from concurrent.futures import ThreadPoolExecutor
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _kernels(n):
+    # wave_kernel<N, KS, PH>: the Schur form (KS = 1, N <= 10) in its one-phase (PH = 0), parking
+    # (1) and resuming (2) instantiations; the Riccati form (KS = 0)
+    schur = [f"wave_kernelILi{n}ELi1ELi{ph}E" for ph in (0, 1, 2)] if n <= 10 else []
+    return schur + [f"wave_kernelILi{n}ELi0ELi0E", f"scale_kernelILi{n}E"]
+
+
 def _check(n):
-    kernels = ([f"wave_kernelILi{n}ELi1E"] if n <= 10 else []) + [f"wave_kernelILi{n}ELi0E", f"scale_kernelILi{n}E"]
+    kernels = _kernels(n)
     cmd = [sys.executable, os.path.join(REPO, "tools", "isa_hazards.py"), "--n", str(n), "--kernels"] + kernels
     return subprocess.run(cmd, capture_output=True, text=True, timeout=1200)
 
@@ -25,4 +33,4 @@ def test_product_kernels_have_no_isa_hazards():
         outs = list(ex.map(_check, horizons))
     for n, o in zip(horizons, outs):
         assert o.returncode == 0, f"N={n}:\n{o.stdout[-3000:]}{o.stderr[-2000:]}"
-        assert o.stdout.count("hazards none") == (3 if n <= 10 else 2), f"N={n}:\n{o.stdout}"
+        assert o.stdout.count("hazards none") == len(_kernels(n)), f"N={n}:\n{o.stdout}"
