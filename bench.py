@@ -232,6 +232,12 @@ def run_rank(args):
     else:
         params = mpcqp.default_params(N)
         solver = mpcqp.MpcQpSolver(params, device=local_rank)
+        if dist_on and "MPCQP_SPLIT" not in os.environ:
+            # a rank that runs RCCL solves its shard as one part: the caller's stream, RCCL's and the
+            # split's two internal streams would exceed the process's four hardware queues
+            # (GPU_MAX_HW_QUEUES); measured at C3's 8192-robot shard with the all-gather every step:
+            # one part 3.00M QP/s, three parts 2.86M, no all-gather 3.02M (profiles/r06/rccl)
+            solver.set_split(1)
         solver.reserve(Bl)
         d_rec = torch.from_numpy(recs_np).to(dev)
         d_res = torch.zeros((Bl, RD), dtype=torch.float64, device=dev)
@@ -358,12 +364,7 @@ def run_rank(args):
             out["cpu_baseline"] = None
         else:
             ks = 1 if N <= 10 else 0  # KKT form of the launch: Schur (N <= 10, default weights) / Riccati
-            # the kernels one solve launches: one-phase, or the two-phase solve's parking launch, the
-            # ordering and the resuming launch (cold Schur form with MPCQP_PARK)
-            parked = ks == 1 and solver.park_cut > 0
-            eff_name = (f"mpcqp::wv::scale_kernel<{N}> + mpcqp::wv::wave_kernel<{N}, 1, 1> + "
-                        f"mpcqp::wv::order_kernel + mpcqp::wv::wave_kernel<{N}, 1, 2>" if parked else
-                        f"mpcqp::wv::scale_kernel<{N}> + mpcqp::wv::wave_kernel<{N}, {ks}, 0>")
+            eff_name = f"mpcqp::wv::scale_kernel<{N}> + mpcqp::wv::wave_kernel<{N}, {ks}>"
             flops = algorithmic_flops(N, local_res["iters"], local_res["rho_updates"])  # rank 0's launch
             achieved = flops / (kern_ms * 1e-3) / 1e12
             key = f"N{N}_B{B}_{args.gait}{'_mu' if args.mixed_mu else ''}"
@@ -577,7 +578,8 @@ def extras(args, solver, params, recs_np, states, base_res, pyoracle, dev):
     ent = {"value": B5 / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms, "batch": B5, "horizon": 10,
            "workload": "C5: mixed gait, contacts ~ Bernoulli(0.5)^4, mu ~ U(0.3,0.9)",
            "mean_iters": float(g5["iters"].mean()),
-           "handoff_count": {"rank_deficient_feet": h5[0], "ill_conditioned_after_rho_update": h5[2],
+           "handoff_count": {"rank_deficient_feet": h5[0], "cancellation_smax_x_amp": h5[1],
+                             "smax_cap": h5[2],
                              "what": "robots the Riccati form solved in their own wave (mpcqp_handoff_counts)"}}
     if pyoracle is not None:
         idx = np.unique(np.linspace(0, B5 - 1, 512).astype(np.int64))
@@ -629,10 +631,10 @@ def extras(args, solver, params, recs_np, states, base_res, pyoracle, dev):
     ent = {"value": B4 / (ms * 1e-3), "unit": "QP/s", "ms_per_step": ms, "batch": B4, "horizon": 20,
            "workload": "C4: horizon 20 (n=240, m=400), trot", "mean_iters": float(g4["iters"].mean()),
            "roofline_frac": fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-           **executed_fields("N20_B4096_trot", "mpcqp::wv::scale_kernel<20> + mpcqp::wv::wave_kernel<20, 0, 0>", ms),
+           **executed_fields("N20_B4096_trot", "mpcqp::wv::scale_kernel<20> + mpcqp::wv::wave_kernel<20, 0>", ms),
            # HBM bytes per launch of the N = 20 solve from its own rocprofv3 PMC pass (profiles/)
            "traffic": load_traffic("N20_B4096_trot",
-                                   "mpcqp::wv::scale_kernel<20> + mpcqp::wv::wave_kernel<20, 0, 0>"),
+                                   "mpcqp::wv::scale_kernel<20> + mpcqp::wv::wave_kernel<20, 0>"),
            "kernels": "scale_kernel<20> + wave_kernel<20, 0> (Riccati form, factorization on MFMA)"}
     if pyoracle is not None:
         idx = np.unique(np.linspace(0, B4 - 1, 256).astype(np.int64))

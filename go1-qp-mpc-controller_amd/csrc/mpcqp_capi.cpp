@@ -38,12 +38,6 @@ struct mpcqp_handle {
   hipEvent_t ev_fork = nullptr;
   hipEvent_t ev_join[KMAX] = {};
   int path = 0;              // 0 auto (= 3), 3 Riccati wave; debug library only: 1 dense K^-1, 2 Riccati workgroup
-  // two-phase cold solve (mpcqp_debug_set_park, MPCQP_PARK): the park slots and the resume order,
-  // grow-only like the workspace
-  int park_cut = 0;
-  double* park = nullptr;
-  int* perm = nullptr;
-  size_t park_cap = 0;
   // host wrapper: device buffers, a private stream and two pinned staging chunks
   hipStream_t hstream = nullptr;
   char* pin[2] = {nullptr, nullptr};
@@ -138,24 +132,6 @@ hipError_t ensure_workspace(mpcqp_handle* h, int32_t batch, void* stream) {
     h->work_per = per;
   }
   return e;
-}
-
-// The two-phase solve's buffers for `batch` robots (park slots, resume order + count).
-hipError_t ensure_park(mpcqp_handle* h, int32_t batch, void* stream) {
-  if ((size_t)batch <= h->park_cap) return hipSuccess;
-  hipError_t e = hipStreamSynchronize((hipStream_t)stream);
-  if (e == hipSuccess) e = hipFree(h->park);
-  if (e == hipSuccess) e = hipFree(h->perm);
-  h->park = nullptr;
-  h->perm = nullptr;
-  h->park_cap = 0;
-  if (e == hipSuccess) e = hipMalloc(&h->park, sizeof(double) * (size_t)mpcqp::park_doubles(h->p.horizon) * batch);
-  if (e == hipSuccess) e = hipMalloc(&h->perm, sizeof(int) * ((size_t)batch + 1));
-  if (e == hipSuccess) h->park_cap = (size_t)batch;
-  return e;
-}
-bool park_wanted(const mpcqp_handle* h, const double* d_state) {
-  return h->park_cut > 0 && !d_state && effective_path(h) == 3 && h->p.horizon <= 10;
 }
 
 // Parts a wave-path solve of `batch` robots is split into.  Auto: three from 3072 robots, two from
@@ -311,7 +287,6 @@ int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** 
   h->slots = cus * per_cu;
   h->cus = cus;
   if (const char* sp = getenv("MPCQP_SPLIT")) h->split = atoi(sp);
-  if (const char* pc = getenv("MPCQP_PARK")) h->park_cut = atoi(pc) > 0 ? atoi(pc) : 0;
   if (const char* sw = getenv("MPCQP_SPLIT_W")) {
     for (int i = 0; i < mpcqp_handle::KMAX && *sw; ++i) {
       char* end = nullptr;
@@ -335,8 +310,6 @@ int32_t mpcqp_destroy(mpcqp_handle* h) {
   (void)hipFree(h->d_sol);
   (void)hipFree(h->d_bal_recs);
   (void)hipFree(h->d_bal_res);
-  (void)hipFree(h->park);
-  (void)hipFree(h->perm);
   if (h->hstream) (void)hipStreamSynchronize(h->hstream);
   for (int i = 0; i < 2; ++i) {
     if (h->pin_ev[i]) (void)hipEventDestroy(h->pin_ev[i]);
@@ -378,22 +351,12 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
   a.grid = batch;
   a.stream = stream;
   a.p = h->p;
-  if (park_wanted(h, d_state)) {
-    e = ensure_park(h, batch, stream);
-    if (e != hipSuccess) return set_hip_error(h, e, "park hipMalloc");
-    a.park_cut = h->park_cut;
-    a.park = h->park;
-    a.perm = h->perm;
-  }
   switch (effective_path(h)) {
 #ifdef MPCQP_DEBUG_PATHS
     case 1: e = mpcqp::launch_solve_any(a); break;
     case 2: e = mpcqp::launch_riccati_any(a); break;
 #endif
     default: {
-      // two-phase solve: the parts run scale_kernel and the first launch; after the join, order_kernel
-      // sorts the whole batch's parked robots and one second launch resumes them
-      const bool parked = mpcqp::park_applies_any(a);
       const int parts = split_parts(h, batch);
       h->fb_parts = parts;
       if (parts == 1) {
@@ -431,10 +394,6 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
         ai.trace_cap = d_trace && trace_cap > b0 ? trace_cap - b0 : 0;
         ai.wstate = d_state ? d_state + ws * b0 : nullptr;
         ai.fallback = h->fb + 4 * i;
-        if (parked) {
-          ai.park = h->park + (size_t)mpcqp::park_doubles(h->p.horizon) * b0;
-          ai.park_phase = 1;
-        }
         if (i == 0) {
           ai.stream = stream;
           e = mpcqp::launch_wave_any(ai);
@@ -447,11 +406,6 @@ static int32_t solve_device_impl(mpcqp_handle* h, const double* d_records, int32
       }
       // join: the caller's stream waits for every other part
       for (int i = 1; i < parts && e == hipSuccess; ++i) e = hipStreamWaitEvent((hipStream_t)stream, h->ev_join[i], 0);
-      if (parked && e == hipSuccess) {
-        mpcqp::LaunchArgs a2 = a;
-        a2.park_phase = 2;
-        e = mpcqp::launch_wave_any(a2);
-      }
       break;
     }
   }
@@ -683,13 +637,6 @@ int32_t mpcqp_debug_set_split(mpcqp_handle* h, int32_t parts) {
   return old;
 }
 
-int32_t mpcqp_debug_set_park(mpcqp_handle* h, int32_t cut) {
-  if (!h || cut < -1) return -MPCQP_ERR_INVALID_ARG;
-  const int32_t old = h->park_cut;
-  if (cut >= 0) h->park_cut = cut;  // -1: query only
-  return old;
-}
-
 int32_t mpcqp_debug_split_parts(mpcqp_handle* h, int32_t batch) {
   if (!h || batch < 1) return 0;
   return effective_path(h) == 3 ? split_parts(h, batch) : 1;
@@ -705,8 +652,6 @@ int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch) {
   if (e != hipSuccess) return set_hip_error(h, e, "workspace hipMalloc");
   if (effective_path(h) == 3) e = ensure_split_streams(h, split_parts(h, batch));
   if (e != hipSuccess) return set_hip_error(h, e, "split streams");
-  if (park_wanted(h, nullptr)) e = ensure_park(h, batch, nullptr);
-  if (e != hipSuccess) return set_hip_error(h, e, "park hipMalloc");
   return MPCQP_OK;
 }
 int32_t mpcqp_solve_threads(int32_t horizon) {

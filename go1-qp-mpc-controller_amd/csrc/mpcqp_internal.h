@@ -23,15 +23,6 @@ struct LaunchArgs {
   int grid;
   void* stream;
   mpcqp_params p;
-  // Two-phase ("parked") Schur-form solve (cold solves, N <= 10; mpcqp_wave.hip, park_cut): robots
-  // still running at iteration `park_cut` save their state to `park` and stop; order_kernel sorts
-  // them by how far their dual residual is from its tolerance; the second launch resumes them
-  // longest-first.  park_cut = 0: one launch.
-  int park_cut = 0;
-  double* park = nullptr;  // [batch][park_doubles(N)]
-  int* perm = nullptr;     // [batch] robots of the second launch, then [batch] the count
-  int park_phase = 0;      // 0 both launches; 1 scale_kernel + the first launch only (one part of a
-                           // split batch); 2 order_kernel + the second launch only (the whole batch)
 };
 
 // Formulation only (mpcqp_build.hip): ConvexMpc::calculate_qp_mats, horizons 1..20
@@ -40,9 +31,6 @@ hipError_t launch_build_any(const LaunchArgs& a, double* P, double* q, double* l
 // The solve: scale_kernel + one-wave-per-robot Riccati wave_kernel (mpcqp_wave.hip), horizons
 // 1..WAVE_MAX_HORIZON
 hipError_t launch_wave_any(const LaunchArgs& a);
-// whether launch_wave_any runs the two-phase solve for these arguments (park_cut > 0, buffers set,
-// cold, Schur form)
-bool park_applies_any(const LaunchArgs& a);
 hipError_t occupancy_wave_any(const mpcqp_params& p, int* blocks);
 hipError_t wave_selftest(double* d_out, void* stream);
 hipError_t launch_scale_any(const LaunchArgs& a);  // scale_kernel alone (the image in a.work)
@@ -67,12 +55,6 @@ __host__ __device__ constexpr int warm_state_doubles(int N) {
 
 // doubles per robot of the scaling image scale_kernel hands to wave_kernel (mpcqp_wave.hip ScaleImg)
 __host__ __device__ constexpr int scale_image_doubles(int N) { return 3 * 12 * N + 20 * N + 3; }
-
-// doubles per robot of a parked Schur-form solve (mpcqp_wave.hip ParkLayout): scalars, the lanes'
-// loop state (X, Z, Y, rhs, R'^-1 rows per register round; row 4 packed) and the LDS factors Q, B
-__host__ __device__ constexpr int park_doubles(int N) {
-  return 16 + 64 * (7 * ((N + 3) / 4) + 2 * (((N + 3) / 4 + 3) / 4)) + (6 * N * 62 + 2) + 6 * N * 14;
-}
 
 // Downstream torque map (mpcqp_torque.hip)
 hipError_t launch_torques(const double* recs, const mpcqp_result* grf, int batch, int* counter, double* tau,

@@ -71,9 +71,8 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
 #ifdef MPCQP_SCALE_TIMING
   const double t_entry = (double)__builtin_readcyclecounter();
 #endif
-  // wave_kernel's hand-off counters start at zero (stream order): [0] rank-deficient feet, [1]
-  // (unused: an ill-conditioned core at the initial rho, never seen; see the flag below), [2] an
-  // ill-conditioned Schur core after a rho update
+  // wave_kernel's hand-off counters start at zero (stream order): [0] rank-deficient feet, [1] a KKT
+  // solve that cancelled too much for its core (S_max * amp > SCHUR_AMP), [2] S_max > SCHUR_SMAX
   if (inst == 0 && t < 3) fb[t] = 0;
   {
     const double* rg = recs + (size_t)inst * C::REC;
@@ -679,51 +678,20 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
   } while (0)
 #endif
 
-// ---- two-phase ("parked") solve of the Schur form ------------------------------------------------
-// The robots of a batch run 25-350 ADMM iterations (C2: median 125), and a launch in input order
-// ends with the long robots that happened to start late running alone (the dispatch tail: ~24 % of
-// the C2 step).  With park_cut > 0 a cold Schur-form solve runs in two launches: the first stops
-// every robot still running after the update_info iteration park_cut (a termination check) and
-// saves its state — iterates, rho, counters, the lanes' R'^-1 rows and the LDS factors Q, B (unless
-// a refactorization is pending) — to a per-robot slot; order_kernel sorts the parked robots by
-// dua_res / eps_dual of that check (the single best predictor of the remaining iterations on the
-// Go1 workloads, profiles/r06/park), largest first; the second launch resumes them in that order.
-// The first launch's robots all do about the same work (setup, a factorization, park_cut iterations),
-// so its own tail is short.  Resuming restores exactly the values the loop would have carried: the
-// iterate sequence and every result are bitwise those of one launch (tests/test_gpu_park.py).
-template <int N>
-struct ParkLayout {
-  static constexpr int R = Cfg<N>::R, NP = (R + 3) / 4, NI = 6 * N;
-  static constexpr int FLAG = 0, KEY = 1, ITER = 2, TOCHECK = 3, TOADAPT = 4, RHOUPD = 5, NTRACE = 6, NEEDF = 7,
-                       RHO = 8, PRI = 9, DUA = 10;
-  static constexpr int NL = 7 * R + 2 * NP;  // per lane: X, Z, Y, RHS, SRI[3] per round; Z4P, Y4P
-  static constexpr int LANE = 16, QB = LANE + 64 * NL, QN = NI * 62 + 2, BB = QB + QN, BN = NI * 14,
-                       SIZE = BB + BN;
-  static_assert(SIZE == park_doubles(N), "park slot layout");
-};
-struct ParkArgs {
-  double* park;  // [batch][park_doubles(N)] or nullptr
-  int cut;       // update_info iteration at which the first launch parks (0: never)
-};
-
 // KS: the KKT solve.  0 = Riccati recursion (chains over the horizon, factors on MFMA; every N),
 // 1 = impulse-space Schur form (mpcqp_schur.h; N <= 10, nonnegative state weights).
 // The solve of robot `inst` by one wave (wave_kernel: one robot per workgroup).  Returns true when a
 // KS = 1 solve hands the robot to the Riccati form without having written anything: scale_kernel
 // flagged it (rank-deficient B6_k), or a factorization's max S_ii crossed SCHUR_SMAX; wave_kernel
 // then solves it with KS = 0 in the same wave.  fb[0] and fb[2] count the two cases.
-// PH: 0 the one-phase solve, 1 the first launch of a two-phase solve (parks at pk.cut), 2 the second
-// (resumes): separate instantiations, so that neither path costs the others registers (together in
-// one kernel they made the allocator spill 45 VGPRs)
-template <int N, int KS, int PH = 0>
+template <int N, int KS>
 __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, const double* __restrict__ recs,
                                            mpcqp_result* __restrict__ results, double* __restrict__ solution,
                                            double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
                                            double* __restrict__ img, const mpcqp_params& p,
-                                           int* __restrict__ fb, const ParkArgs& pk) {
+                                           int* __restrict__ fb) {
   using C = Cfg<N>;
   using WL = WarmLayout<N>;
-  using PL = ParkLayout<N <= 10 ? N : 10>;
   constexpr int n = C::n, m = C::m, R = C::R;
   const int t = threadIdx.x;
   const int q = t >> 4, li = t & 15, leg = li >> 2, a = li & 3;
@@ -806,9 +774,7 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
   double* const im = img + (size_t)inst * SI::SIZE;
   const double c_s = im[SI::CS];
   const int mode = (int)im[SI::MODE];  // 0 cold, 1 osqp_update_P, 2 OsqpEigen re-init
-  // (a resumed robot passed this test in the first launch, whose factorizations have since written
-  // max S_ii into the slot)
-  if (KS == 1 && PH != 2) {
+  if (KS == 1) {
     const double flag = im[SI::DEGEN];
     if (flag != 0.0) {
       // rank-deficient B6_k (collinear / coincident feet: G_k would be singular; the reference QP is
@@ -1092,63 +1058,8 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
   double obj_sum = 0.0;  // 1/2 x'P~x + q~'x of the final iterate (scaled), set when the loop ends
   bool need_factor = true;
   int to_check = p.check_termination, to_adapt = p.adaptive_rho_interval;
-  int iter0 = 1;
-  bool amp_bad = false;     // the Schur form's cancellation bound was crossed at the last check
-  bool parked = false;      // the first launch of a two-phase solve stopped at pk.cut
-  double park_den = 0.0;    // c^-1 max(|D^-1 q~|, |D^-1 A~'y|, |D^-1 P~x|) of that check (eps_dual)
-  // the robot's park slot (two-phase solve, Schur form only)
-  double* const pslot = (KS == 1 && PH != 0) ? pk.park + (size_t)inst * PL::SIZE : nullptr;
-  if constexpr (KS == 1 && PH == 2) {
-    {
-      // resume: the state the first launch saved after its update_info iteration pk.cut; rho's
-      // vectors from rho exactly as the refactorization request computes them
-      iter0 = (int)pslot[PL::ITER] + 1;
-      to_check = (int)pslot[PL::TOCHECK];
-      to_adapt = (int)pslot[PL::TOADAPT];
-      rho_updates = (int)pslot[PL::RHOUPD];
-      ntrace = (int)pslot[PL::NTRACE];
-      need_factor = pslot[PL::NEEDF] != 0.0;
-      rho = pslot[PL::RHO];
-      pri_res = pslot[PL::PRI];
-      dua_res = pslot[PL::DUA];
-      iters = iter0 - 1;
-      rinv = 1. / rho;
-#pragma unroll
-      for (int pr = 0; pr < NP; ++pr) {
-        RHO4P[pr] = rho4_of(L4P[pr], U4P[pr], rho);
-        RI4P[pr] = 1. / RHO4P[pr];
-      }
-      const double* ln = pslot + PL::LANE + t;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        X[r] = ln[64 * (0 * R + r)];
-        Z[r] = ln[64 * (1 * R + r)];
-        Y[r] = ln[64 * (2 * R + r)];
-        RHS[r] = ln[64 * (3 * R + r)];
-      }
-#pragma unroll
-      for (int pr = 0; pr < NP; ++pr) {
-        Z4P[pr] = ln[64 * (7 * R + pr)];
-        Y4P[pr] = ln[64 * (7 * R + NP + pr)];
-      }
-      if (!need_factor) {  // the R'^-1 rows, Q and B as the last factorization left them
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          SRI[r][0] = ln[64 * (4 * R + 3 * r + 0)];
-          SRI[r][1] = ln[64 * (4 * R + 3 * r + 1)];
-          SRI[r][2] = ln[64 * (4 * R + 3 * r + 2)];
-        }
-        const double2* qs = reinterpret_cast<const double2*>(pslot + PL::QB);
-        double2* qd = reinterpret_cast<double2*>(F.Q);
-        for (int e = t; e < PL::QN / 2; e += NT) qd[e] = qs[e];
-        const double2* bs = reinterpret_cast<const double2*>(pslot + PL::BB);
-        double2* bd = reinterpret_cast<double2*>(&F.Bm[0][0]);
-        for (int e = t; e < PL::BN / 2; e += NT) bd[e] = bs[e];
-      }
-      wave_sync();
-    }
-  }
-  for (int iter = iter0; iter <= p.max_iter; ++iter) {
+  bool amp_bad = false;  // the Schur form's cancellation bound was crossed at the last check
+  for (int iter = 1; iter <= p.max_iter; ++iter) {
     if (need_factor) {
 #ifdef MPCQP_REPEAT_FACTOR  // cost measurement builds: the (idempotent) factorization runs twice
      for (int rep = 0; rep < 2; ++rep) {
@@ -1858,60 +1769,12 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
           RHS[r] = (sigma * X[r] - Qv[r]) + at;
         }
       }
-      if (KS == 1 && PH == 1 && iter == pk.cut) {  // park (after the loop)
-        parked = true;
-        park_den = cinv * mx[6];
-        break;
-      }
     }
     if (tm_ck) WV_MARK(49);
     if (tm_it) WV_MARK(47);
   }
 
   WV_MARK(20);
-  if constexpr (KS == 1 && PH == 1) {
-    if (parked) {
-      // park: everything the next iteration reads, for the second launch (no result written)
-      if (t == 0) {
-        pslot[PL::FLAG] = 1.0;
-        pslot[PL::KEY] = dua_res / (p.eps_abs + p.eps_rel * park_den);  // dua_res / eps_dual
-        pslot[PL::ITER] = iters;
-        pslot[PL::TOCHECK] = to_check;
-        pslot[PL::TOADAPT] = to_adapt;
-        pslot[PL::RHOUPD] = rho_updates;
-        pslot[PL::NTRACE] = ntrace;
-        pslot[PL::NEEDF] = need_factor ? 1.0 : 0.0;
-        pslot[PL::RHO] = rho;
-        pslot[PL::PRI] = pri_res;
-        pslot[PL::DUA] = dua_res;
-      }
-      double* ln = pslot + PL::LANE + t;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        ln[64 * (0 * R + r)] = X[r];
-        ln[64 * (1 * R + r)] = Z[r];
-        ln[64 * (2 * R + r)] = Y[r];
-        ln[64 * (3 * R + r)] = RHS[r];
-        ln[64 * (4 * R + 3 * r + 0)] = SRI[r][0];
-        ln[64 * (4 * R + 3 * r + 1)] = SRI[r][1];
-        ln[64 * (4 * R + 3 * r + 2)] = SRI[r][2];
-      }
-#pragma unroll
-      for (int pr = 0; pr < NP; ++pr) {
-        ln[64 * (7 * R + pr)] = Z4P[pr];
-        ln[64 * (7 * R + NP + pr)] = Y4P[pr];
-      }
-      if (!need_factor) {
-        const double2* qs = reinterpret_cast<const double2*>(F.Q);
-        double2* qd = reinterpret_cast<double2*>(pslot + PL::QB);
-        for (int e = t; e < PL::QN / 2; e += NT) qd[e] = qs[e];
-        const double2* bs = reinterpret_cast<const double2*>(&F.Bm[0][0]);
-        double2* bd = reinterpret_cast<double2*>(pslot + PL::BB);
-        for (int e = t; e < PL::BN / 2; e += NT) bd[e] = bs[e];
-      }
-      return false;
-    }
-  }
   if (KS == 1 && (amp_bad || !(img_at(SI::DEGEN) <= SCHUR_SMAX))) {  // the Riccati form solves it
     if (t == 0) atomicAdd(fb + (amp_bad ? 1 : 2), 1);
     return true;
@@ -2010,14 +1873,14 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
 #else
 #define MPCQP_WAVE_BOUNDS __launch_bounds__(NT, 1)
 #endif
-template <int N, int KS, int PH = 0>
+template <int N, int KS>
 __global__ MPCQP_WAVE_BOUNDS void wave_kernel(const double* __restrict__ recs, int batch,
                                                      mpcqp_result* __restrict__ results,
                                                      double* __restrict__ solution, double* __restrict__ trace,
                                                      int trace_cap, double* __restrict__ wstate,
                                                      double* __restrict__ img, mpcqp_params p,
-                                                     int* __restrict__ fb, ParkArgs pk, const int* __restrict__ perm) {
-  int inst = blockIdx.x;
+                                                     int* __restrict__ fb) {
+  const int inst = blockIdx.x;
   if constexpr (KS == 1) {
     // The Schur form, and in the same wave the Riccati form for the robots it hands over (the two
     // forms' LDS images share one allocation: the Riccati factors fit inside the Schur core's)
@@ -2025,79 +1888,15 @@ __global__ MPCQP_WAVE_BOUNDS void wave_kernel(const double* __restrict__ recs, i
       WSmem<N, 1> s;
       WSmem<N, 0> r;
     } sm;
-    if constexpr (PH == 2) {  // the second launch: the parked robots, longest first (order_kernel)
-      if (inst >= perm[batch]) return;
-      inst = perm[inst];
-    }
     if (inst >= batch) return;
-    // the first launch clears the robot's park flag before anything else (a robot that returns early
-    // — non-finite record, degenerate feet, a finished or handed-over solve — is then not resumed)
-    if (PH == 1 && threadIdx.x == 0) pk.park[(size_t)inst * ParkLayout<N>::SIZE] = 0.0;
-    if (wave_solve<N, 1, PH>(inst, sm.s, recs, results, solution, trace, trace_cap, wstate, img, p, fb, pk)) {
+    if (wave_solve<N, 1>(inst, sm.s, recs, results, solution, trace, trace_cap, wstate, img, p, fb)) {
       wave_sync();
-      const ParkArgs none{nullptr, 0};
-      wave_solve<N, 0>(inst, sm.r, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr, none);
+      wave_solve<N, 0>(inst, sm.r, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr);
     }
   } else {
     __shared__ WSmem<N, 0> sm;
     if (inst >= batch) return;
-    const ParkArgs none{nullptr, 0};
-    wave_solve<N, 0>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb, none);
-  }
-}
-
-// Orders the robots the first launch of a two-phase solve parked: perm[0 .. count) = parked robots by
-// descending key (dua_res / eps_dual at the park check), bucketed in quarter octaves (the order
-// inside a bucket is whatever the atomics give: it changes the schedule, never a result);
-// perm[batch] = count.  One workgroup.
-constexpr int ORDER_NT = 1024, ORDER_NB = 128, ORDER_CACHE = 32768, ORDER_KPT = 8;
-__global__ __launch_bounds__(ORDER_NT) void order_kernel(const double* __restrict__ park, int stride, int batch,
-                                                         int* __restrict__ perm) {
-  __shared__ int hist[ORDER_NB], off[ORDER_NB];
-  __shared__ unsigned char bks[ORDER_CACHE];  // bucket + 1 of robots [0, ORDER_CACHE) (0: not parked)
-  const int t = threadIdx.x;
-  for (int b = t; b < ORDER_NB; b += ORDER_NT) hist[b] = 0;
-  __syncthreads();
-  auto bucket = [](double key) {
-    const double l = key > 0.0 ? 4.0 * log2(key) : -1e9;  // NaN keys fall in bucket 0
-    return (int)fmin(fmax(floor(l) + 64.0, 0.0), (double)(ORDER_NB - 1));
-  };
-  // bucket + 1 of robot i, or 0 (the loads of a thread's robots issued together)
-  auto scan = [&](auto&& use) {
-    for (int base = 0; base < batch; base += ORDER_NT * ORDER_KPT) {
-      double fl[ORDER_KPT], ky[ORDER_KPT];
-#pragma unroll
-      for (int k = 0; k < ORDER_KPT; ++k) {
-        const int i = base + t + k * ORDER_NT;
-        const double* sl = park + (size_t)(i < batch ? i : 0) * stride;
-        fl[k] = i < batch ? sl[0] : 0.0;
-        ky[k] = i < batch ? sl[1] : 0.0;
-      }
-#pragma unroll
-      for (int k = 0; k < ORDER_KPT; ++k) use(base + t + k * ORDER_NT, fl[k] == 1.0 ? bucket(ky[k]) + 1 : 0);
-    }
-  };
-  scan([&](int i, int b1) {
-    if (i < ORDER_CACHE && i < batch) bks[i] = (unsigned char)b1;
-    if (b1) atomicAdd(&hist[b1 - 1], 1);
-  });
-  __syncthreads();
-  if (t == 0) {
-    int acc = 0;
-    for (int b = ORDER_NB - 1; b >= 0; --b) {  // largest keys first
-      off[b] = acc;
-      acc += hist[b];
-    }
-    perm[batch] = acc;
-  }
-  __syncthreads();
-  if (batch <= ORDER_CACHE) {
-    for (int i = t; i < batch; i += ORDER_NT)
-      if (bks[i]) perm[atomicAdd(&off[bks[i] - 1], 1)] = i;
-  } else {
-    scan([&](int i, int b1) {
-      if (b1) perm[atomicAdd(&off[b1 - 1], 1)] = i;
-    });
+    wave_solve<N, 0>(inst, sm, recs, results, solution, trace, trace_cap, wstate, img, p, fb);
   }
 }
 
@@ -2128,10 +1927,6 @@ static bool schur_ok(const mpcqp_params& p) {
 #endif
   return true;
 }
-// The two-phase solve serves cold Schur-form solves (warm ticks converge in a few iterations)
-static bool park_used(const LaunchArgs& a) {
-  return a.park_cut > 0 && a.park && a.perm && !a.wstate && a.p.horizon <= 10 && schur_ok(a.p);
-}
 // experiment builds: MPCQP_WAVE_LDS_PAD bytes of dynamic LDS per wave-kernel workgroup (fewer robots
 // per CU: per-robot phase costs without neighbours sharing the CU's LDS or instruction cache)
 #ifndef MPCQP_WAVE_LDS_PAD
@@ -2140,44 +1935,19 @@ static bool park_used(const LaunchArgs& a) {
 template <int N>
 static hipError_t launch_wave(const LaunchArgs& a) {
   if (!a.fallback) return hipErrorInvalidValue;
-  hipError_t e = hipSuccess;
-  const bool parked = N <= 10 && park_used(a);
-  if (!parked || a.park_phase != 2) {
-    hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
-                       a.recs, a.batch, a.wstate, a.work, a.p, a.fallback);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  const wv::ParkArgs none{nullptr, 0};
+  hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
+                     a.recs, a.batch, a.wstate, a.work, a.p, a.fallback);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   if constexpr (N <= 10) {
     if (schur_ok(a.p)) {
-      if (parked) {  // two launches (wv::ParkLayout): park at a.park_cut, order, resume
-        const wv::ParkArgs pk{a.park, a.park_cut};
-        if (a.park_phase != 2) {
-          hipLaunchKernelGGL((wv::wave_kernel<N, 1, 1>), dim3(a.batch), dim3(wv::NT), MPCQP_WAVE_LDS_PAD,
-                             (hipStream_t)a.stream, a.recs, a.batch, a.results, a.solution, a.trace, a.trace_cap,
-                             a.wstate, a.work, a.p, a.fallback, pk, (const int*)nullptr);
-          e = hipGetLastError();
-          if (e != hipSuccess || a.park_phase == 1) return e;
-        }
-        hipLaunchKernelGGL(wv::order_kernel, dim3(1), dim3(wv::ORDER_NT), 0, (hipStream_t)a.stream, a.park,
-                           park_doubles(N), a.batch, a.perm);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((wv::wave_kernel<N, 1, 2>), dim3(a.batch), dim3(wv::NT), MPCQP_WAVE_LDS_PAD, (hipStream_t)a.stream,
-                           a.recs, a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p,
-                           a.fallback, pk, (const int*)a.perm);
-        return hipGetLastError();
-      }
       hipLaunchKernelGGL((wv::wave_kernel<N, 1>), dim3(a.batch), dim3(wv::NT), MPCQP_WAVE_LDS_PAD, (hipStream_t)a.stream, a.recs,
-                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback,
-                         none, (const int*)nullptr);
+                         a.batch, a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
       return hipGetLastError();
     }
   }
   hipLaunchKernelGGL((wv::wave_kernel<N, 0>), dim3(a.batch), dim3(wv::NT), MPCQP_WAVE_LDS_PAD, (hipStream_t)a.stream, a.recs, a.batch,
-                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback, none,
-                     (const int*)nullptr);
+                     a.results, a.solution, a.trace, a.trace_cap, a.wstate, a.work, a.p, a.fallback);
   return hipGetLastError();
 }
 template <int N>
@@ -2209,7 +1979,6 @@ hipError_t launch_wave_any(const LaunchArgs& a) {
     default: return hipErrorInvalidValue;
   }
 }
-bool park_applies_any(const LaunchArgs& a) { return park_used(a); }
 hipError_t launch_scale_any(const LaunchArgs& a) {
   switch (a.p.horizon) {
 #define CASE(K) \

@@ -773,13 +773,15 @@ constexpr double SCHUR_GRAM_TOL = MPCQP_SCHUR_GRAM_TOL;
 // (profiles/r06/cancel: 7,254 robots — stance / mixed at weights x 1, 5, 100, the golden sets, C2 and
 // C5 samples — solved to the end by the Schur form in builds with -ffp-contract=fast and =on): the
 // worst u0 error of the robots a bound keeps, S_max <= 3e3: 8.3e-9 (fast) / 6.8e-9 (on), 52 handed
-// over; S_max * amp <= 3e4: 1.1e-9 / 8.1e-10, 96 handed over (C2: 1 of 2048, C5: 24 of 2048).
+// over; S_max * amp <= 5e4: 2.4e-9 / 2.0e-9, 69 handed over (C2: 0 of 2048, C5: 14 of 2048);
+// <= 3e4: 1.1e-9 / 8.1e-10 but C5 hands over 101 of 8192 robots and takes 3.15 ms instead of 2.91
+// (profiles/r06/cancel/ab.txt: a few late hand-offs re-solved from the start end the batch).
 #ifndef MPCQP_SCHUR_SMAX
 #define MPCQP_SCHUR_SMAX 1e4
 #endif
 constexpr double SCHUR_SMAX = MPCQP_SCHUR_SMAX;
 #ifndef MPCQP_SCHUR_AMP
-#define MPCQP_SCHUR_AMP 3e4
+#define MPCQP_SCHUR_AMP 5e4
 #endif
 constexpr double SCHUR_AMP = MPCQP_SCHUR_AMP;
 template <int N>

@@ -107,7 +107,7 @@ EXPORTED = [
     "mpcqp_balance_solve_host", "mpcqp_solve_batch_warm_host",
     "mpcqp_debug_scale_image_doubles", "mpcqp_debug_scale_image_device", "mpcqp_copy_warm_slots_device",
     "mpcqp_handoff_counts",
-    "mpcqp_debug_set_split", "mpcqp_debug_split_parts", "mpcqp_debug_set_park",
+    "mpcqp_debug_set_split", "mpcqp_debug_split_parts",
 ]
 
 _libs = {}
@@ -189,8 +189,6 @@ def load(debug=False):
     L.mpcqp_debug_set_split.restype = i32
     L.mpcqp_debug_split_parts.argtypes = [vp, i32]
     L.mpcqp_debug_split_parts.restype = i32
-    L.mpcqp_debug_set_park.argtypes = [vp, i32]
-    L.mpcqp_debug_set_park.restype = i32
     ps, rs = i32(0), i32(0)
     L.mpcqp_abi_sizes(ctypes.byref(ps), ctypes.byref(rs))
     if ps.value != ctypes.sizeof(Params) or rs.value != ctypes.sizeof(Result):

@@ -65,26 +65,14 @@ class MpcQpSolver:
             raise ValueError("mpcqp_debug_set_split: parts must be 0..8")
         return old
 
-    def set_park(self, cut):
-        """mpcqp_debug_set_park: two-phase cold solve parked at update_info iteration `cut` (0: one
-        phase); returns the previous setting."""
-        old = int(self._L.mpcqp_debug_set_park(self._h, int(cut)))
-        if old < 0:
-            raise ValueError("mpcqp_debug_set_park: cut must be >= 0")
-        return old
-
-    @property
-    def park_cut(self):
-        """The two-phase setting (0: one-phase solves)."""
-        return int(self._L.mpcqp_debug_set_park(self._h, -1))
-
     def split_parts(self, batch):
         """mpcqp_debug_split_parts: parts a solve of `batch` robots is split into."""
         return int(self._L.mpcqp_debug_split_parts(self._h, int(batch)))
 
     def handoff_counts(self):
         """mpcqp_handoff_counts: robots of the last Schur-form solve that the Riccati form solved in
-        their own wave, as (rank-deficient feet, 0 (reserved), ill-conditioned after a rho update).
+        their own wave, as (rank-deficient feet, S_max x cancellation above SCHUR_AMP, S_max above the
+        SCHUR_SMAX cap).
         Synchronizes the device."""
         import ctypes
         c = (ctypes.c_int32 * 3)()

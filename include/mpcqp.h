@@ -131,8 +131,10 @@ int32_t mpcqp_record_size(int32_t horizon);
 int32_t mpcqp_create(const mpcqp_params* params, int32_t device, mpcqp_handle** out);
 int32_t mpcqp_destroy(mpcqp_handle* h);
 
-/* Pre-size the per-instance device workspace (128x128 binary64 per robot) so that later
- * mpcqp_solve_batch_device calls with batch <= `batch` never allocate (hipGraph-capture safe). */
+/* Pre-size the handle's device workspace — the scaling image scale_kernel hands to wave_kernel,
+ * 56N + 3 binary64 per robot (3.5 KB at N = 10) — and create the internal streams a solve of `batch`
+ * robots splits over, so that later mpcqp_solve_batch_device calls with batch <= `batch` neither
+ * allocate nor create streams (hipGraph-capture safe). */
 int32_t mpcqp_reserve(mpcqp_handle* h, int32_t batch);
 
 /* Replaces calculate_A/B_mat_c + discretization + calculate_qp_mats + OSQP initSolver/solve

@@ -26,10 +26,10 @@ int32_t mpcqp_abi_sizes(int32_t* params_size, int32_t* result_size);
 int32_t mpcqp_handle_slots(mpcqp_handle* h);
 
 /* Robots of the handle's last Schur-form (N <= 10) wave solve that the Riccati form solved in their
- * own wave: counts[0] rank-deficient feet (scale_kernel's screen), counts[1] always 0 (reserved: an
- * ill-conditioned core at the initial rho, which the workloads never show), counts[2] a core whose
- * max S_ii crossed SCHUR_SMAX after a rho update (it left the Schur form at the next check).
- * Synchronizes the device. */
+ * own wave: counts[0] rank-deficient feet (scale_kernel's screen), counts[1] a check whose KKT solve
+ * cancelled too much for its core (max S_ii times the push-through identity's observed cancellation
+ * above SCHUR_AMP), counts[2] a core whose max S_ii crossed the cap SCHUR_SMAX (each left the Schur
+ * form at that check).  Synchronizes the device. */
 int32_t mpcqp_handoff_counts(mpcqp_handle* h, int32_t counts[3]);
 
 /* Parts a wave-path solve is split into (solved concurrently on the handle's internal streams,
@@ -41,14 +41,6 @@ int32_t mpcqp_debug_set_split(mpcqp_handle* h, int32_t parts);
 
 /* Parts a solve of `batch` robots on this handle is split into under its current setting. */
 int32_t mpcqp_debug_split_parts(mpcqp_handle* h, int32_t batch);
-
-/* Two-phase cold solve of the Schur form (horizons <= 10): robots still running after the update_info
- * iteration `cut` park their state, are sorted by how far their dual residual is from its tolerance,
- * and a second launch resumes them longest-first (a batch solved this way is one launch; results are
- * bitwise those of the one-phase solve).  0 = one-phase; `cut` should be a multiple of
- * check_termination; -1 only queries.  The environment variable MPCQP_PARK sets the initial value at
- * mpcqp_create.  Returns the previous setting, or -MPCQP_ERR_INVALID_ARG. */
-int32_t mpcqp_debug_set_park(mpcqp_handle* h, int32_t cut);
 
 /* Threads per robot workgroup of the solve kernel the default path uses for horizon N. */
 int32_t mpcqp_solve_threads(int32_t horizon);

@@ -1,8 +1,9 @@
 """Ill-conditioned Schur cores (mpcqp_schur.h, the hand-off): with four feet in contact and state
 weights a few times the Go1 defaults, S = I + L'CL gets large and the push-through identity
 R'^-1 w - B'(I - S^-1)B w loses digits (u0 off the oracle by up to 1e-3 at x 100, round-4 fuzz,
-profiles/r04/smax).  A robot whose core crosses SCHUR_SMAX (after a rho update: at the initial rho
-none does) leaves the Schur form at the next check and is solved again by the Riccati form in its
+profiles/r04/smax).  A robot leaves the Schur form at a check when the latest factorization's max S_ii
+times that iteration's observed cancellation (schur_solve's amp = max|R'^-1 w| / max|u|) exceeds
+SCHUR_AMP = 5e4, or S_max exceeds SCHUR_SMAX = 1e4, and is solved again by the Riccati form in its
 own wave (wave_kernel).
 Gates: status and iterations equal to the oracle, u0 within SURVEY §8(c)'s 1e-4, and a regression
 sentinel at the accuracy the hand-off achieves."""
@@ -33,11 +34,11 @@ def test_heavy_state_weights_match_oracle(oracle, gait, scale):
     np.testing.assert_array_equal(got["iters"], ref["iters"])
     err = rel_err_u0(got["u0"], ref["u0"])
     assert np.all(err <= 1e-4), float(err.max())
-    # regression sentinel: the hand-off keeps these within ~1e-6 (without it 1.4e-5 at x1 stance,
-    # 4e-4 at x5, 1e-3 at x100)
-    sentinel(err, 1e-5 if gait == "stance" or scale > 1 else 1e-8, f"conditioning {gait} x{scale:g}")
+    # regression sentinel: the hand-off (S_max * amp > 5e4 or S_max > 1e4) keeps these within ~2.5e-9
+    # (without it 1.4e-5 at x1 stance, 5e-5 at x5, 1e-3 at x100; profiles/r06/cancel)
+    sentinel(err, 1e-8, f"conditioning {gait} x{scale:g}")
     if gait == "stance":
-        assert counts[2] > 0  # the hand-off is exercised here
+        assert counts[1] + counts[2] > 0  # the hand-off is exercised here
 
 
 @pytest.mark.parametrize("N", [3, 6, 10])
@@ -57,7 +58,7 @@ def test_heavy_weights_shorter_horizons(oracle, N):
     np.testing.assert_array_equal(got["iters"], ref["iters"])
     err = rel_err_u0(got["u0"], ref["u0"])
     assert np.all(err <= 1e-4), float(err.max())
-    sentinel(err, 1e-5, f"conditioning N={N} stance x20")
+    sentinel(err, 1e-8, f"conditioning N={N} stance x20")
 
 
 def test_heavy_weights_warm_ticks(oracle):
@@ -93,5 +94,7 @@ def test_heavy_weights_warm_ticks(oracle):
         err = rel_err_u0(out[t]["u0"], ref[t]["u0"])
         assert np.all(err <= 1e-4), f"tick {t}"
         worst = max(worst, float(err.max()))
-    sentinel(np.array([worst]), 1e-5, "conditioning warm ticks x100")
+    # (warm-started ticks keep the previous tick's adapted rho: round 6 measured 2.2e-7 here with the
+    # S_max * amp hand-off, as with round 5's S_max bound; the cold heavy-weight cases above reach 1e-9)
+    sentinel(np.array([worst]), 1e-6, "conditioning warm ticks x100")
     assert handed > 0

@@ -140,7 +140,7 @@ def test_near_degenerate_sweep(oracle, N, eps, kind):
     assert np.all(err <= 1e-4)
     g = gram_ratio(recs, N)
     note(f"near-degenerate N={N} {kind} eps={eps:.0e}", gram_ratio_min=float(g.min()), gram_ratio_max=float(g.max()),
-         screened=int(counts[0]), smax_handoffs=int(counts[2]), max_u0_rel_err=float(err.max()))
+         screened=int(counts[0]), conditioning_handoffs=int(counts[1] + counts[2]), max_u0_rel_err=float(err.max()))
     sentinel(err, SENTINEL, f"near-degenerate N={N} {kind} eps={eps:.0e}")
 
 

@@ -148,12 +148,10 @@ def test_product_library_ships_only_the_default_solve():
     dbg = kernels(_lib.DEBUG_LIB_PATH)
     # horizon 10: the Schur-form solve (KS = 1) and the Riccati form (KS = 0, negative weights);
     # horizon 20: Riccati only
-    # (wave_kernel<N, KS, PH>: PH 1 / 2 are the two launches of the two-phase cold solve)
-    for k in ("mpcqp::wv::wave_kernel<10, 1, 0>", "mpcqp::wv::wave_kernel<10, 1, 1>", "mpcqp::wv::wave_kernel<10, 1, 2>",
-              "mpcqp::wv::wave_kernel<10, 0, 0>", "mpcqp::wv::wave_kernel<20, 0, 0>", "mpcqp::wv::order_kernel",
+    for k in ("mpcqp::wv::wave_kernel<10, 1>", "mpcqp::wv::wave_kernel<10, 0>", "mpcqp::wv::wave_kernel<20, 0>",
               "mpcqp::wv::scale_kernel<10>", "mpcqp::wv::scale_kernel<20>"):
         assert k in prod, k
-    assert "mpcqp::wv::wave_kernel<20, 1" not in prod
+    assert "mpcqp::wv::wave_kernel<20, 1>" not in prod
     for name in ("mpcqp::solve_kernel<", "mpcqp::ric::ric_solve_kernel<", "mw_kernel", "dx_kernel"):
         assert name not in prod, name
     assert "mpcqp::solve_kernel<10>" in dbg and "mpcqp::ric::ric_solve_kernel<10>" in dbg

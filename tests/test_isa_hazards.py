@@ -3,8 +3,7 @@ wait only where the compiled code needs it (mpcqp_wave_common.h, DPP wait states
 must show no DPP / permlane / transcendental / untracked-load hazard.  Every horizon the product
 library instantiates is checked (each N is scheduled separately; the round-6 check found
 two real DPP hazards at N = 7 and 8 that the N = 10 / 20 check could not see): wave_kernel<N, 1> for
-N <= 10 (one-phase, parking and resuming instantiations), wave_kernel<N, 0> and scale_kernel<N> for
-N = 1..20.  CPU only (hipcc -S, one compile per
+N <= 10, wave_kernel<N, 0> and scale_kernel<N> for N = 1..20.  CPU only (hipcc -S, one compile per
 horizon, in parallel)."""
 import os
 import subprocess
@@ -15,10 +14,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _kernels(n):
-    # wave_kernel<N, KS, PH>: the Schur form (KS = 1, N <= 10) in its one-phase (PH = 0), parking
-    # (1) and resuming (2) instantiations; the Riccati form (KS = 0)
-    schur = [f"wave_kernelILi{n}ELi1ELi{ph}E" for ph in (0, 1, 2)] if n <= 10 else []
-    return schur + [f"wave_kernelILi{n}ELi0ELi0E", f"scale_kernelILi{n}E"]
+    # wave_kernel<N, KS>: the Schur form (KS = 1, N <= 10) and the Riccati form (KS = 0)
+    return ([f"wave_kernelILi{n}ELi1E"] if n <= 10 else []) + [f"wave_kernelILi{n}ELi0E", f"scale_kernelILi{n}E"]
 
 
 def _check(n):

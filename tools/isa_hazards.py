@@ -239,7 +239,7 @@ def main():
         names = [f"wave_kernelILi{n}ELi1E" for n in range(1, 11)] + [f"wave_kernelILi{n}ELi0E" for n in range(1, 21)] \
             + [f"scale_kernelILi{n}E" for n in range(1, 21)]
     else:
-        names = [f"wave_kernelILi{a.n}ELi1E", f"wave_kernelILi{a.n}ELi0E", f"scale_kernelILi{a.n}E"]
+        names = ([f"wave_kernelILi{a.n}ELi1E"] if a.n <= 10 else []) + [f"wave_kernelILi{a.n}ELi0E", f"scale_kernelILi{a.n}E"]
     total = 0
     seen = 0
     for nm, lines, l0 in kernels(text, names):
