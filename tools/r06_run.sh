@@ -18,7 +18,7 @@ grep -E "^FAILED|passed|failed" "$OUT/gpu_tests.txt" | tail -12
 if [ -n "$BASE" ]; then
   timeout -k 10 200 python3 tools/ab_bitwise.py dump "$OUT/ab_new.npz" > "$OUT/ab.txt" 2>&1
   MPCQP_LIB=$PWD/exp/$BASE.so timeout -k 10 200 python3 tools/ab_bitwise.py dump "$OUT/ab_base.npz" >> "$OUT/ab.txt" 2>&1
-  python3 tools/ab_bitwise.py cmp "$OUT/ab_base.npz" "$OUT/ab_new.npz" | tee -a "$OUT/ab.txt"
+  python3 tools/ab_bitwise.py cmp "$OUT/ab_base.npz" "$OUT/ab_new.npz" >> "$OUT/ab.txt" || true; tail -3 "$OUT/ab.txt"
   rm -f "$OUT"/ab_*.npz
 fi
 timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
