@@ -34,6 +34,11 @@
 // Arithmetic is binary64 throughout.
 #include "mpcqp_schur.h"
 
+// OSQP scale_data inside the Schur-form wave (scale_wave) instead of a scale_kernel launch before it
+#ifndef MPCQP_FUSED_SCALE
+#define MPCQP_FUSED_SCALE 0
+#endif
+
 namespace mpcqp {
 namespace wv {
 
@@ -643,6 +648,486 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
 }
 #undef SC_MARK
 
+// ---- OSQP scale_data inside the robot's own wave (fused setup, N <= 10) ---------------------------
+// scale_kernel's computation on the 64 lanes of the Schur-form wave instead of a separate two-wave
+// launch: lane t owns columns t and t + 64 of P~ (CPT slots) and rows t + 64 r of A~; the gradient
+// sweeps run on lanes 0-12, then the degenerate-feet screen on lanes 16 .. 16 + N - 1.  Every value is
+// computed by the same expressions, and the two block reductions of the exact passes add the two
+// column slots' wave sums in scale_kernel's wave order, so the image is bitwise scale_kernel's
+// (tests/test_gpu_fused.py).  The image is still written for the checks' D / E reloads and for a
+// Riccati hand-off; the setup's copies (D, q~, the raw gradient, E) are left in the LDS image.
+struct FusedScale {
+  double c_s;
+  int mode;
+  bool degen;
+};
+template <int N>
+__device__ __forceinline__ FusedScale scale_wave(WSmem<N, 1>& sm, const mpcqp_params& p, double* __restrict__ wstate,
+                                                 int inst, const Adisc& A, double dtm, double mu,
+                                                 double* __restrict__ out) {
+  using C = Cfg<N>;
+  using WL = WarmLayout<N>;
+  using SI = ScaleImg<N>;
+  constexpr int n = C::n, m = C::m, CPT = (n + 63) / 64, RPT = (m + 63) / 64, BPT = N;
+  auto& H = sm.u.h;
+  const int t = threadIdx.x;
+  const double* rec = H.rec;
+  const double dt = A.dt;
+  // -- gradient sweeps (scale_kernel wave 0) and the Gram screen (scale_kernel wave 1) --
+  double Iwinv[9];
+  iw_inverse(rec, Iwinv);
+  {
+    if (t < SD) H.vec[0][t] = rec[MPCQP_REC_X0 + t];
+    double q2t = 2 * p.q_weights[t < ND ? t : 0];
+    keep(q2t);
+    const int tr = t < SD ? t : 0;
+    const int fj1 = tr <= 1 ? 6 : (tr == 2 ? 8 : (tr <= 5 ? tr + 6 : (tr == 11 ? 12 : tr)));
+    const double fc1 = tr == 0 ? A.ad0 : (tr == 1 ? -A.ad1 : ((tr <= 5 || tr == 11) ? dt : 0.0));
+    const int fj2 = tr <= 1 ? 7 : tr;
+    const double fc2 = tr == 0 ? A.ad1 : (tr == 1 ? A.ad0 : 0.0);
+    const int bj1 = tr == 6 || tr == 7 ? 0 : (tr == 8 ? 2 : (tr >= 9 && tr < ND ? tr - 6 : tr));
+    const double bc1 = tr == 6 ? A.ad0 : (tr == 7 ? A.ad1 : ((tr >= 8 && tr < ND) ? dt : 0.0));
+    const int bj2 = tr == 6 || tr == 7 ? 1 : tr;
+    const double bc2 = tr == 6 ? -A.ad1 : (tr == 7 ? A.ad0 : 0.0);
+    wave_sync();
+    for (int i = 0; i < N; ++i) {
+      if (t < SD) {
+        const double* pv = H.vec[i & 1];
+        const double sv = fma(fc2, pv[fj2], fma(fc1, pv[fj1], pv[tr]));
+        H.vec[(i + 1) & 1][t] = sv;
+        if (t < ND) H.lam[i][t] = q2t * (sv - rec[MPCQP_REC_XREF + SD * i + t]);
+      }
+      wave_sync();
+    }
+    for (int j = N - 2; j >= 0; --j) {
+      if (t < ND) {
+        const double* v = H.lam[j + 1];
+        H.lam[j][t] = H.lam[j][t] + fma(bc2, v[bj2], fma(bc1, v[bj1], v[tr]));
+      }
+      wave_sync();
+    }
+  }
+  bool any_degen;
+  {
+    int degen = 0;
+    if (t >= 16 && t < 16 + N) {
+      const int k = t - 16;
+      double bw[3][ND];
+#pragma unroll
+      for (int lg = 0; lg < 4; ++lg) {
+        const double* fp = rec + MPCQP_REC_FEET(N) + 12 * k + 3 * lg;
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+          const double i0 = Iwinv[3 * rr], i1 = Iwinv[3 * rr + 1], i2 = Iwinv[3 * rr + 2];
+          bw[rr][3 * lg + 0] = (i1 * fp[2] - i2 * fp[1]) * dt;
+          bw[rr][3 * lg + 1] = (i2 * fp[0] - i0 * fp[2]) * dt;
+          bw[rr][3 * lg + 2] = (i0 * fp[1] - i1 * fp[0]) * dt;
+        }
+      }
+      double G[21];
+      auto gi = [](int r1, int r2) { return r1 * (r1 + 1) / 2 + r2; };
+#pragma unroll
+      for (int r1 = 0; r1 < 6; ++r1)
+#pragma unroll
+        for (int r2 = 0; r2 <= r1; ++r2) {
+          double g = 0.0;
+          if (r1 < 3) {
+#pragma unroll
+            for (int b = 0; b < ND; ++b) g += bw[r1][b] * bw[r2][b];
+          } else if (r2 < 3) {
+#pragma unroll
+            for (int l = 0; l < 4; ++l) g += bw[r2][3 * l + (r1 - 3)] * dtm;
+          } else {
+            g = r1 == r2 ? 4.0 * dtm * dtm : 0.0;
+          }
+          G[gi(r1, r2)] = g;
+        }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const double d0 = G[gi(c, c)];
+        double sc = d0;
+#pragma unroll
+        for (int e = 0; e < c; ++e) sc -= G[gi(c, e)] * G[gi(c, e)];
+        degen |= !(sc > SCHUR_GRAM_TOL * d0);
+        const double dg = sqrt(dmax(sc, 0.0)), di = dg > 0.0 ? 1.0 / dg : 0.0;
+        G[gi(c, c)] = dg;
+#pragma unroll
+        for (int r1 = c + 1; r1 < 6; ++r1) {
+          double v = G[gi(r1, c)];
+#pragma unroll
+          for (int e = 0; e < c; ++e) v -= G[gi(r1, e)] * G[gi(c, e)];
+          G[gi(r1, c)] = v * di;
+        }
+      }
+    }
+    any_degen = __any(degen) != 0;
+  }
+  // -- columns (CPT slots per lane) and rows: gradient, D = E = 1, the friction pyramid --
+  double* Dc = H.D;
+  double* Ec = H.E;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int j0 = t + 64 * c;
+    if (j0 < n) {
+      const int k = j0 / ND, ii = j0 % ND;
+      const double* lm = H.lam[k];
+      const double g = ((sm.Bw[k][0][ii] * lm[6] + sm.Bw[k][1][ii] * lm[7]) + sm.Bw[k][2][ii] * lm[8]) + dtm * lm[9 + ii % 3];
+      H.q[j0] = g;
+      H.qn[j0] = g;
+      Dc[j0] = 1.0;
+    }
+  }
+  for (int r = t; r < m; r += 64) {
+    Ec[r] = 1.0;
+    const int a5 = r % 5;  // friction pyramid rows (ConvexMpc.cpp:46-58)
+    H.Ap[0][r] = a5 < 4 ? 1.0 : 0.0;
+    H.Ap[1][r] = a5 < 4 ? ((a5 & 1) ? -mu : mu) : 1.0;
+  }
+  wave_sync();
+  double* const ws = wstate ? wstate + (size_t)inst * WL::SIZE : nullptr;
+  const bool had = ws && ws[WL::FLAG] != 0.0;
+  auto colmax1 = [&](int j0, bool first) __attribute__((always_inline)) -> double {
+    (void)first;
+    double mx0 = 0.0, mx1 = 0.0;
+    if (j0 < n)
+      gen_col<N, BPT, false>(sm, p, A, dtm, j0, 0, [&](int, int b, int ri, double hv) __attribute__((always_inline)) {
+        if (b & 1) mx1 = fmax(mx1, Dc[ri] * dabs(hv));
+        else mx0 = fmax(mx0, Dc[ri] * dabs(hv));
+      });
+    return fmax(mx0, mx1);
+  };
+  auto pattern1 = [&](int j0) __attribute__((always_inline)) -> bool {
+    unsigned long long zm[WL::MW];
+#pragma unroll
+    for (int w = 0; w < WL::MW; ++w) zm[w] = 0ull;
+    auto put = [&](int, int, int ri, double hv) __attribute__((always_inline)) {
+      const unsigned long long bit = (hv == 0.0 && ri <= j0) ? (1ull << (ri & 63)) : 0ull;
+#pragma unroll
+      for (int w = 0; w < WL::MW; ++w) zm[w] |= (ri >> 6) == w ? bit : 0ull;
+    };
+    bool diff = false;
+    if (j0 < n) {
+      gen_col<N, BPT, false>(sm, p, A, dtm, j0, 0, put);
+      double* slot = ws + WL::MASK + WL::MW * j0;
+#pragma unroll
+      for (int w = 0; w < WL::MW; ++w) {
+        diff |= __double_as_longlong(slot[w]) != (long long)zm[w];
+        slot[w] = __longlong_as_double((long long)zm[w]);
+      }
+    }
+    return diff;
+  };
+  auto acol = [&](int j) __attribute__((always_inline)) {
+    const int f = j / 3, aa = j % 3;
+    const double* e = Ec + 5 * f;
+    const double* a0 = H.Ap[0] + 5 * f;
+    const double* a1 = H.Ap[1] + 5 * f;
+    const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4];
+    const double m0 = dmax(e0 * dabs(a0[0]), e1 * dabs(a0[1]));
+    const double m1 = dmax(e2 * dabs(a0[2]), e3 * dabs(a0[3]));
+    const double m2 = dmax(dmax(dmax(dmax(dabs(a1[0]) * e0, dabs(a1[1]) * e1), dabs(a1[2]) * e2), dabs(a1[3]) * e3),
+                           e4 * dabs(a1[4]));
+    return sel3(aa, m0, m1, m2) * Dc[j];
+  };
+  auto arow = [&](int r) __attribute__((always_inline)) {
+    const int f = r / 5, k5 = r % 5;
+    const double e = Ec[r];
+    const double* d = Dc + 3 * f;
+    const double a0r = H.Ap[0][r], a1r = H.Ap[1][r], dk = d[k5 < 4 ? k5 >> 1 : 0], d2 = d[2];
+    const double m4 = (e * dabs(a1r)) * d2;
+    const double m03 = dmax((e * dabs(a0r)) * dk, (dabs(a1r) * e) * d2);
+    return k5 == 4 ? m4 : m03;
+  };
+  double c_s = 1.0, cm[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) cm[c] = 0.0;
+  bool pattern_changed = false;
+  bool cm_ub = true;
+#ifndef MPCQP_SCALE_EXACT_CM0
+  for (int i = 0; i < ND; ++i) cm_ub = cm_ub && p.q_weights[i] >= 0.0 && p.r_weights[i % MPCQP_NUM_DOF] >= 0.0;
+#else
+  cm_ub = false;
+#endif
+  if (p.scaling > 0 || ws) {
+    if (cm_ub) {  // colmax_ub: max_i |H_ij| <= sqrt(H_jj max_i H_ii)
+      double hd[CPT], hm = 0.0;
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const int j0 = t + 64 * c;
+        hd[c] = 0.0;
+        if (j0 < n) {
+          const int a2 = j0 % ND;
+          double h = 0.0;
+          gen_col<N, 1, true>(sm, p, A, dtm, j0, j0 / ND, [&](int, int b, int, double hv) __attribute__((always_inline)) {
+            h = b == a2 ? hv : h;
+          });
+          hd[c] = h;
+        }
+        hm = fmax(hm, hd[c]);
+      }
+      hm = wave_max(hm);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) cm[c] = sqrt(dmax(hd[c], 0.0) * hm) * (1.0 + 0x1p-20);
+    } else {
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) cm[c] = colmax1(t + 64 * c, true);
+    }
+    if (ws) {
+      bool d = false;
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) d |= pattern1(t + 64 * c);
+      pattern_changed = __any(d) != 0;
+    }
+  }
+  const bool mu_changed = had && ws[WL::MU] != mu;
+  const int mode = !had ? 0 : ((pattern_changed || mu_changed) ? 2 : 1);
+  if (mode == 1) {
+    const double cinv_o = 1. / ws[WL::C];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int j0 = t + 64 * c;
+      if (j0 < n) H.q[j0] = (1. / ws[WL::D + j0]) * (cinv_o * ws[WL::QT + j0]);
+    }
+    for (int r = t; r < m; r += 64) {
+      const int f = r / 5, k5 = r % 5;
+      const double ei = 1. / ws[WL::E + r];
+      const double d2 = 1. / ws[WL::D + 3 * f + 2];
+      H.Ap[0][r] = k5 < 4 ? (ws[WL::AK + r] * ei) * (1. / ws[WL::D + 3 * f + (k5 >> 1)]) : 0.0;
+      H.Ap[1][r] = (ws[WL::AK + m + r] * ei) * d2;
+    }
+    wave_sync();
+  }
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int j0 = t + 64 * c;
+    if (j0 < n) H.cm0[j0] = cm[c];
+  }
+  wave_sync();
+  if (cm_ub && p.scaling > 0) {
+    bool wins = false;
+    if (t < 4 * N) {
+      const double* a0 = H.Ap[0] + 5 * t;
+      const double* a1 = H.Ap[1] + 5 * t;
+      const double* cz = H.cm0 + 3 * t;
+      const double m0 = dmax(Ec[5 * t] * dabs(a0[0]), Ec[5 * t + 1] * dabs(a0[1]));
+      const double m1 = dmax(Ec[5 * t + 2] * dabs(a0[2]), Ec[5 * t + 3] * dabs(a0[3]));
+      const double m2 = dmax(dmax(dmax(dmax(dabs(a1[0]) * Ec[5 * t], dabs(a1[1]) * Ec[5 * t + 1]),
+                                       dabs(a1[2]) * Ec[5 * t + 2]), dabs(a1[3]) * Ec[5 * t + 3]),
+                             Ec[5 * t + 4] * dabs(a1[4]));
+      wins = !(cz[0] <= m0 * Dc[3 * t]) || !(cz[1] <= m1 * Dc[3 * t + 1]) || !(cz[2] <= m2 * Dc[3 * t + 2]);
+    }
+    if (__any(wins)) {
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const int j0 = t + 64 * c;
+        cm[c] = colmax1(j0, true);
+        if (j0 < n) H.cm0[j0] = cm[c];
+      }
+      wave_sync();
+    }
+  }
+  int pass = 0;
+  bool resume = false;
+  {
+    constexpr int NF = 4 * N;
+    constexpr double EPS = 2.220446049250313e-16;
+    constexpr double M1 = 1.0 + 4.0 * (n + 8) * EPS;
+    constexpr double M2 = 1.0 + 16.0 * EPS;
+    double dmax_prev = 1.0;
+    for (; pass < p.scaling; ++pass) {
+      double s0 = 0.0, qm = 0.0, dm = 0.0, rmin = INFINITY, moved = 0.0;
+      if (t < NF) {
+        const int f = t;
+        double e[5], a0[5], a1[5], d[3], cz[3];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          e[i] = Ec[5 * f + i];
+          a0[i] = H.Ap[0][5 * f + i];
+          a1[i] = H.Ap[1][5 * f + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          d[i] = Dc[3 * f + i];
+          cz[i] = H.cm0[3 * f + i];
+        }
+        auto acol3 = [&](const double (&ee)[5], double (&mc)[3]) __attribute__((always_inline)) {
+          mc[0] = dmax(ee[0] * dabs(a0[0]), ee[1] * dabs(a0[1]));
+          mc[1] = dmax(ee[2] * dabs(a0[2]), ee[3] * dabs(a0[3]));
+          mc[2] = dmax(dmax(dmax(dmax(dabs(a1[0]) * ee[0], dabs(a1[1]) * ee[1]), dabs(a1[2]) * ee[2]),
+                            dabs(a1[3]) * ee[3]),
+                       ee[4] * dabs(a1[4]));
+        };
+        double mc[3];
+        acol3(e, mc);
+        double dtv[3], et[5];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const double cmj = pass == 0 ? cz[i] : dmax_prev * cz[i];
+          const double pc = (c_s * d[i]) * cmj;
+          dtv[i] = limit_scaling(fmax(pc, mc[i] * d[i]));
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          const double dk = d[i < 4 ? i >> 1 : 0], d2 = d[2];
+          const double m4 = (e[i] * dabs(a1[i])) * d2;
+          const double m03 = dmax((e[i] * dabs(a0[i])) * dk, (dabs(a1[i]) * e[i]) * d2);
+          et[i] = limit_scaling(i == 4 ? m4 : m03);
+        }
+        bool ne1 = false;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) ne1 |= dtv[i] != 1.0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) ne1 |= et[i] != 1.0;
+        if (__any(ne1)) {
+#pragma unroll
+          for (int i = 0; i < 3; ++i) dtv[i] = 1.0 / sqrt(dtv[i]);
+#pragma unroll
+          for (int i = 0; i < 5; ++i) et[i] = 1.0 / sqrt(et[i]);
+        }
+        moved = ne1 ? 1.0 : 0.0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          e[i] = e[i] * et[i];
+          Ec[5 * f + i] = e[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const double qj = dtv[i] * H.q[3 * f + i];
+          H.q[3 * f + i] = qj;
+          d[i] = d[i] * dtv[i];
+          Dc[3 * f + i] = d[i];
+          s0 += (c_s * d[i]) * cz[i];
+          qm = dmax(qm, dabs(qj));
+          dm = dmax(dm, d[i]);
+        }
+        acol3(e, mc);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const double den = d[i] * cz[i];
+          rmin = fmin(rmin, den > 0.0 ? (mc[i] * d[i]) / den : INFINITY);
+        }
+      }
+      // (scale_kernel: the same wave reductions, then + the second wave's partials, all neutral: its
+      // lanes hold no foot)
+      s0 = wave_sum(s0) + 0.0;
+      qm = dmax(wave_max(qm), 0.0);
+      dm = dmax(wave_max(dm), 0.0);
+      rmin = fmin(-wave_max(-rmin), INFINITY);
+      moved = dmax(wave_max(moved), 0.0);
+      wave_sync();
+      const double inf_norm_q = limit_scaling(qm);
+      const double c_temp = 1. / limit_scaling(inf_norm_q);
+      const double c_new = c_s * c_temp;
+      const bool ok1 = ((dm * s0) * M1) / n <= inf_norm_q;
+      const bool ok2 = pass + 1 == p.scaling || (c_new * dm) * M2 <= rmin;
+      if (!(ok1 && ok2)) {
+        resume = true;
+        break;
+      }
+      if (t < NF) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) H.q[3 * t + i] *= c_temp;
+      }
+      const bool fixed = moved == 0.0 && c_temp == 1.0 && dm == dmax_prev;
+      c_s = c_new;
+      dmax_prev = dm;
+      if (fixed) {
+        pass = p.scaling;
+        break;
+      }
+    }
+  }
+  // exact passes: H's columns regenerated for the norms
+  for (; pass < p.scaling; ++pass) {
+    if (!resume) {
+      double dtv[CPT];
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const int j0 = t + 64 * c;
+        dtv[c] = 1.0;
+        if (j0 < n) {
+          const double pc = (c_s * Dc[j0]) * cm[c];
+          dtv[c] = 1.0 / sqrt(limit_scaling(fmax(pc, acol(j0))));
+        }
+      }
+      double et[RPT];
+#pragma unroll
+      for (int rr = 0; rr < RPT; ++rr) {
+        const int r = t + 64 * rr;
+        et[rr] = r < m ? 1.0 / sqrt(limit_scaling(arow(r))) : 1.0;
+      }
+      double* const Dn = Dc == H.D ? H.Dx : H.D;
+      double* const En = Ec == H.E ? H.Ex : H.E;
+#pragma unroll
+      for (int rr = 0; rr < RPT; ++rr) {
+        const int r = t + 64 * rr;
+        if (r < m) En[r] = Ec[r] * et[rr];
+      }
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const int j0 = t + 64 * c;
+        if (j0 < n) {
+          H.q[j0] = dtv[c] * H.q[j0];
+          Dn[j0] = Dc[j0] * dtv[c];
+        }
+      }
+      Dc = Dn;
+      Ec = En;
+    }
+    resume = false;
+    wave_sync();
+    // cost normalization: the column slots' wave sums added in scale_kernel's wave order
+    double sv = 0.0, qv = 0.0;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int j0 = t + 64 * c;
+      cm[c] = colmax1(j0, false);
+      const double svc = j0 < n ? (c_s * Dc[j0]) * cm[c] : 0.0;
+      sv = c == 0 ? wave_sum(svc) : sv + wave_sum(svc);
+      qv = fmax(qv, j0 < n ? dabs(H.q[j0]) : 0.0);
+    }
+    if (CPT == 1) sv = sv + 0.0;  // (scale_kernel adds its second wave's zero partial)
+    qv = wave_max(qv);
+    double c_temp = sv / n;
+    const double inf_norm_q = limit_scaling(qv);
+    c_temp = dmax(c_temp, inf_norm_q);
+    c_temp = limit_scaling(c_temp);
+    c_temp = 1. / c_temp;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int j0 = t + 64 * c;
+      if (j0 < n) H.q[j0] *= c_temp;
+    }
+    c_s *= c_temp;
+  }
+  wave_sync();
+  // the image (the checks reload D and E from it; a Riccati hand-off reads all of it) and, in the
+  // setup image, the final D and E (the passes may have left them in the second buffers)
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int j0 = t + 64 * c;
+    if (j0 < n) {
+      const double dj = Dc[j0];
+      out[SI::D + j0] = dj;
+      out[SI::Q + j0] = H.q[j0];
+      if (ws) out[SI::QN + j0] = H.qn[j0];
+      H.D[j0] = dj;
+    }
+  }
+  for (int r = t; r < m; r += 64) {
+    const double er = Ec[r];
+    out[SI::E + r] = er;
+    H.E[r] = er;
+  }
+  if (t == 0) {
+    out[SI::CS] = c_s;
+    out[SI::MODE] = (double)mode;
+    out[SI::DEGEN] = any_degen ? 1.0 : 0.0;
+  }
+  wave_sync();
+  return FusedScale{c_s, mode, any_degen};
+}
+
 // Phase timing (debug builds with -DMPCQP_PHASE_TIMING): lane 0 of each traced robot appends
 // {phase id, s_memtime, s_memrealtime (100 MHz), 0} to the trace buffer instead of check records.
 #ifdef MPCQP_PHASE_TIMING
@@ -684,7 +1169,8 @@ __global__ __launch_bounds__(ScaleCfg<N>::NTS, ScaleCfg<N>::WPE) void scale_kern
 // KS = 1 solve hands the robot to the Riccati form without having written anything: scale_kernel
 // flagged it (rank-deficient B6_k), or a factorization's max S_ii crossed SCHUR_SMAX; wave_kernel
 // then solves it with KS = 0 in the same wave.  fb[0] and fb[2] count the two cases.
-template <int N, int KS>
+// FUSED (KS = 1): OSQP scale_data runs in this wave (scale_wave) instead of scale_kernel's launch
+template <int N, int KS, bool FUSED = false>
 __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, const double* __restrict__ recs,
                                            mpcqp_result* __restrict__ results, double* __restrict__ solution,
                                            double* __restrict__ trace, int trace_cap, double* __restrict__ wstate,
@@ -768,28 +1254,39 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
 
   WV_MARK(3);
 
-  // ---- 3. OSQP scale_data: the image scale_kernel wrote (D, E, q~, c, branch; raw q if warm) ------
+  // ---- 3. OSQP scale_data: computed here by the robot's wave (fused setup, Schur form), or the image
+  // scale_kernel wrote (D, E, q~, c, branch; raw q if warm) ---------------------------------------
   using SI = ScaleImg<N>;
   // (not const: the Schur form records max S_ii of its latest factorization in the DEGEN slot)
   double* const im = img + (size_t)inst * SI::SIZE;
-  const double c_s = im[SI::CS];
-  const int mode = (int)im[SI::MODE];  // 0 cold, 1 osqp_update_P, 2 OsqpEigen re-init
-  if (KS == 1) {
-    const double flag = im[SI::DEGEN];
-    if (flag != 0.0) {
-      // rank-deficient B6_k (collinear / coincident feet: G_k would be singular; the reference QP is
-      // still strictly convex, R > 0): the Riccati form (KS = 0) solves this robot.  Nothing of it
-      // has been written yet.
-      if (t == 0) atomicAdd(fb, 1);
-      return true;
+  double c_s;
+  int mode;  // 0 cold, 1 osqp_update_P, 2 OsqpEigen re-init
+  bool degen_feet = false;
+  if constexpr (KS == 1 && FUSED) {
+    const FusedScale fs = scale_wave<N>(sm, p, wstate, inst, A, dtm, mu_rec, im);
+    c_s = fs.c_s;
+    mode = fs.mode;
+    degen_feet = fs.degen;  // (D, q~, the raw gradient and E are in the setup image already)
+  } else {
+    c_s = im[SI::CS];
+    mode = (int)im[SI::MODE];
+    if (KS == 1) degen_feet = im[SI::DEGEN] != 0.0;
+  }
+  if (KS == 1 && degen_feet) {
+    // rank-deficient B6_k (collinear / coincident feet: G_k would be singular; the reference QP is
+    // still strictly convex, R > 0): the Riccati form (KS = 0) solves this robot.  Nothing of it
+    // has been written yet (the fused setup wrote the image the Riccati form reads).
+    if (t == 0) atomicAdd(fb, 1);
+    return true;
+  }
+  if (!(KS == 1 && FUSED)) {
+    for (int j = t; j < n; j += NT) {
+      HS.D[j] = im[SI::D + j];
+      HS.q[j] = im[SI::Q + j];
+      if (mode != 0) HS.qn[j] = im[SI::QN + j];
     }
+    for (int r = t; r < m; r += NT) HS.E[r] = im[SI::E + r];
   }
-  for (int j = t; j < n; j += NT) {
-    HS.D[j] = im[SI::D + j];
-    HS.q[j] = im[SI::Q + j];
-    if (mode != 0) HS.qn[j] = im[SI::QN + j];
-  }
-  for (int r = t; r < m; r += NT) HS.E[r] = im[SI::E + r];
   // Warm start (A1RobotControl.h:67 member solver, :522-538): the slot of the previous tick.
   double* const ws = wstate ? wstate + (size_t)inst * WL::SIZE : nullptr;
   // The unscaled constraint entries of row ri (ConvexMpc.cpp:46-58), as scale_kernel used them:
@@ -1889,7 +2386,8 @@ __global__ MPCQP_WAVE_BOUNDS void wave_kernel(const double* __restrict__ recs, i
       WSmem<N, 0> r;
     } sm;
     if (inst >= batch) return;
-    if (wave_solve<N, 1>(inst, sm.s, recs, results, solution, trace, trace_cap, wstate, img, p, fb)) {
+    if (wave_solve<N, 1, MPCQP_FUSED_SCALE != 0>(inst, sm.s, recs, results, solution, trace, trace_cap, wstate, img,
+                                                   p, fb)) {
       wave_sync();
       wave_solve<N, 0>(inst, sm.r, recs, results, solution, trace, trace_cap, wstate, img, p, nullptr);
     }
@@ -1935,9 +2433,14 @@ static bool schur_ok(const mpcqp_params& p) {
 template <int N>
 static hipError_t launch_wave(const LaunchArgs& a) {
   if (!a.fallback) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
-                     a.recs, a.batch, a.wstate, a.work, a.p, a.fallback);
-  hipError_t e = hipGetLastError();
+  hipError_t e = hipSuccess;
+  if (!(MPCQP_FUSED_SCALE && N <= 10 && schur_ok(a.p))) {
+    hipLaunchKernelGGL((wv::scale_kernel<N>), dim3(a.batch), dim3(wv::ScaleCfg<N>::NTS), 0, (hipStream_t)a.stream,
+                       a.recs, a.batch, a.wstate, a.work, a.p, a.fallback);
+    e = hipGetLastError();
+  } else {  // the fused setup: wave_kernel scales; the hand-off counters start at zero (stream order)
+    e = hipMemsetAsync(a.fallback, 0, 4 * sizeof(int), (hipStream_t)a.stream);
+  }
   if (e != hipSuccess) return e;
   if constexpr (N <= 10) {
     if (schur_ok(a.p)) {

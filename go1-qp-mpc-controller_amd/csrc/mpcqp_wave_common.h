@@ -94,6 +94,10 @@ struct WSmem {
       double lam[N][ND];  // gradient adjoint lambda_k (states 0..11)
       double vec[2][16];  // sequential 13-vectors (gradient forward sweep)
       double qn[C::n];     // this tick's gradient (warm start: q of the Ruiz passes is the old one)
+      // OSQP scale_data inside the Schur-form wave (scale_wave, KS = 1 only): the Ruiz passes' second
+      // D / E buffers, the unscaled A entries and the raw column norms (inside the union: no LDS added)
+      static constexpr int FX = KS == 1 ? 1 : 0;
+      double Dx[FX ? C::n : 1], Ex[FX ? C::m : 1], Ap[2][FX ? C::m : 1], cm0[FX ? C::n : 1];
     } h;
     // KS = 0: the Riccati factors; KS = 1: the impulse-space Schur form (mpcqp_schur.h)
     typename std::conditional<KS == 0, RicFactors<N, SACL>, SchurLds<N>>::type f;
