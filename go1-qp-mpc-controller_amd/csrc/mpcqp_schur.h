@@ -27,6 +27,12 @@
 #pragma once
 #include "mpcqp_wave_common.h"
 
+// 1: Q = I - S^-1 by the blocked Gauss-Jordan sweep on the matrix cores (schur_gj_mfma); 0: the
+// in-register scalar sweep (schur_gj_valu)
+#ifndef MPCQP_GJ_MFMA
+#define MPCQP_GJ_MFMA 0
+#endif
+
 namespace mpcqp {
 namespace wv {
 
@@ -181,12 +187,389 @@ __device__ __forceinline__ void rowbcast4(double v, double& c0, double& c1, doub
   c3 = __hiloint2double((int)hb[1], (int)lb[1]);
 }
 
+#if MPCQP_GJ_MFMA
+// ---- blocked Gauss-Jordan on the matrix cores (MPCQP_GJ_MFMA) ------------------------------------
+// S as 16x16 tiles in the MFMA result layout of mpcqp_wave_common.h (tile X[I][J]: lane j + 16 g,
+// register v holds S[16 I + 4 v + g][16 J + j]), in which register kb of a tile is the B operand of
+// K-block kb and, of the transposed tile, the A operand: C += A X takes A' and X as they are.
+
+// x: odd DPP rows <-> y: even rows (permlane16_swap); x: rows 2, 3 <-> y: rows 0, 1 (permlane32_swap)
+__device__ __forceinline__ void swap16d(double& x, double& y) {
+  const auto l = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(x), (unsigned)__double2loint(y), false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(y), false, false);
+  x = __hiloint2double((int)h[0], (int)l[0]);
+  y = __hiloint2double((int)h[1], (int)l[1]);
+}
+__device__ __forceinline__ void swap32d(double& x, double& y) {
+  const auto l = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(x), (unsigned)__double2loint(y), false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(y), false, false);
+  x = __hiloint2double((int)h[0], (int)l[0]);
+  y = __hiloint2double((int)h[1], (int)l[1]);
+}
+// 4x4 (DPP row, register) transpose: afterwards y[r] in row g = y[g] in row r before
+// (tools/mb/mfma_f64_layout.hip checks it)
+__device__ __forceinline__ void transpose_rows(double (&y)[4]) {
+  swap16d(y[0], y[1]);
+  swap16d(y[2], y[3]);
+  swap32d(y[0], y[2]);
+  swap32d(y[1], y[3]);
+}
+
+// a += (lane L's a) * g, one register (GJ_FMA1) or four (GJ_FMA4) per asm block; HEAD: the block
+// may follow the VALU write of a source (2 wait states).  Volatile, so the blocks keep their order:
+// a pivot's first block follows the previous pivot's last one by the next pivot's head block, and the
+// previous pivot's new column (a plain select, which the compiler may sink to its first use) is in
+// the head block.  tools/isa_hazards.py checks the placement.
+#define GJ_F(I) "v_fmac_f64_dpp %[a" #I "], %[a" #I "], %[g] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"
+template <int L, bool HEAD>
+__device__ __forceinline__ void gj_fma1(double& a0, double g) {
+  if constexpr (HEAD)
+    asm volatile("s_nop 1\n\t" GJ_F(0) : [a0] "+v"(a0) : [g] "v"(g), [l] "n"(L));
+  else
+    asm volatile(GJ_F(0) : [a0] "+v"(a0) : [g] "v"(g), [l] "n"(L));
+}
+template <int L, bool HEAD>
+__device__ __forceinline__ void gj_fma4(double& a0, double& a1, double& a2, double& a3, double g) {
+  if constexpr (HEAD)
+    asm volatile("s_nop 1\n\t" GJ_F(0) GJ_F(1) GJ_F(2) GJ_F(3)
+        : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3) : [g] "v"(g), [l] "n"(L));
+  else
+    asm volatile(GJ_F(0) GJ_F(1) GJ_F(2) GJ_F(3)
+        : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3) : [g] "v"(g), [l] "n"(L));
+}
+#undef GJ_F
+// columns of pivot p's row update other than p (overwritten) and p + 1 (updated first), column p - 1
+// first: the previous pivot's last write (its new column) may sit just before the update, so it goes
+// into the block with the wait states
+template <int PV>
+struct GjCols {
+  static constexpr int count(int p) { return PV - 1 - (p + 1 < PV ? 1 : 0); }
+  static constexpr int at(int p, int n) {
+    if (p > 0 && n == 0) return p - 1;
+    int c = 0;
+    for (int k = p > 0 ? 1 : 0;; ++c) {
+      if (c == p || c == p + 1 || c == p - 1) continue;
+      if (k == n) return c;
+      ++k;
+    }
+  }
+};
+// In-place Gauss-Jordan inverse of a symmetric positive definite 16x16 tile in the row layout (lane t
+// of every DPP row holds row t in R[0..15]) whose first PV rows / columns are the matrix and whose pad
+// holds the identity; scalar pivots, no pivoting.  Row p reaches every lane by row_newbcast, so a
+// pivot is one prelude (pivot, reciprocal, the lane's factor) and PV - 1 DPP FMAs.  Software
+// pipelined: column p + 1 is updated first, then the next prelude's dependent chain is issued among
+// the other columns' FMAs.  issue(IC<p>) runs at pivot p (the caller's matrix-core work).
+template <int PV, class Issue>
+__device__ __forceinline__ void gj_rows(double (&R)[16], int li, Issue&& issue) {
+  const double one = 1.0;
+  struct Pv {
+    double g, newc;
+  };
+  auto prelude = [&](auto P) __attribute__((always_inline)) {
+    constexpr int p = decltype(P)::value;
+    Pv o;
+    const double pinv = recip(rbcast<p>(R[p], one));
+    const double cp = R[p] * pinv;
+    o.g = li == p ? pinv - 1.0 : -cp;
+    o.newc = li == p ? pinv : -cp;
+    return o;
+  };
+  Pv cur = prelude(IC<0>{});
+  sfor<0, PV>([&](auto P) __attribute__((always_inline)) {
+    constexpr int p = decltype(P)::value;
+    using C = GjCols<PV>;
+    constexpr int n = C::count(p), n4 = n / 4;
+    // the other columns' blocks: chunk q < n4 four columns, then the single columns
+    auto chunk = [&](auto Q) __attribute__((always_inline)) {
+      constexpr int q = decltype(Q)::value;
+      if constexpr (q < n4) {
+        constexpr int c0 = C::at(p, 4 * q), c1 = C::at(p, 4 * q + 1), c2 = C::at(p, 4 * q + 2), c3 = C::at(p, 4 * q + 3);
+        gj_fma4<p, q == 0>(R[c0], R[c1], R[c2], R[c3], cur.g);
+      }
+    };
+    auto singles = [&]() __attribute__((always_inline)) {
+      sfor<4 * n4, n>([&](auto Q) __attribute__((always_inline)) {
+        constexpr int q = decltype(Q)::value;
+        constexpr int c0 = C::at(p, q);
+        gj_fma1<p, q == 0>(R[c0], cur.g);
+      });
+    };
+    Pv nxt;
+    if constexpr (p + 1 < PV) {
+      gj_fma1<p, true>(R[p + 1], cur.g);
+      nxt = prelude(IC<p + 1>{});
+    }
+    issue(P);
+    sfor<0, n4>(chunk);
+    singles();
+    R[p] = cur.newc;
+    if constexpr (p + 1 < PV) cur = nxt;
+  });
+}
+
+// Q = I - S^-1 by a blocked Gauss-Jordan sweep over 16x16 tiles (NB = ceil(6N / 16) block rows).
+// Step k: P = X_kk^-1 (VALU, gj_rows), X_kj <- P X_kj, X_ij <- X_ij - X_ik X_kj, X_kk <- P (i, j != k;
+// the column panel X_ik <- -X_ik P is implied, below).  The sweep keeps X sign-symmetric,
+// X_ba = s X_ab' with s = -1 when exactly one of blocks a, b has been swept, so one tile per pair
+// {a, b} is kept, in the orientation the sweep needs next: (a, b), a < b, until step b needs row b,
+// which transposes it through LDS (X_ba = -X_ab') and keeps (b, a) from then on.  X_ik enters only as
+// an A operand, i.e. as X_ik' = s X_ki: a step is the row panel X_kj of every j != k and the update
+// of every kept pair (9 chains of NB K-blocks at NB = 4).  The panel and update that produce the next
+// pivot tile go first; the step's other MFMAs are issued among the next tile's pivots (GjPlanSym).
+// Pad K-blocks of a short last block are skipped.
+template <int NB, int k>
+struct GjPlanSym {
+  static constexpr int kn = k + 1 < NB ? k + 1 : -1;  // the next pivot block (its panel went first)
+  // a chain: kind 0 the row panel X_kb -> RP[b], kind 2 the update of kept tile X_ab
+  static constexpr int code(int kind, int a, int b) { return 100 * kind + 10 * a + b; }
+  // the kept orientation of pair {i, j}, i < j, both != k, during step k
+  static constexpr int orient(int i, int j) { return j < k ? code(2, j, i) : code(2, i, j); }
+  // group 1: row panels and the updates whose B operand is the next pivot block's (lookahead) panel;
+  // group 2: the updates that need a group-1 row panel
+  static constexpr int list(int grp, int n) {
+    int m = 0;
+    if (grp == 1)
+      for (int jj = 0; jj < NB; ++jj)
+        if (jj != k && jj != kn) {
+          if (m == n) return code(0, k, jj);
+          ++m;
+        }
+    for (int i = 0; i < NB; ++i)
+      for (int jj = i; jj < NB; ++jj) {
+        if (i == k || jj == k || (i == kn && jj == kn)) continue;
+        const int cd = i == jj ? code(2, i, i) : orient(i, jj);
+        if (((cd % 10) == kn) == (grp == 1)) {
+          if (m == n) return cd;
+          ++m;
+        }
+      }
+    return -1 - m;
+  }
+  static constexpr int count(int grp) { return -1 - list(grp, 1000); }
+};
+
+// S - I in the lane's row (lane t = row t, S[m] = column m; rows and columns NI..63 zero) -> Q in F.Q.
+// pre(): run after the sweep, before the first store to Q (the factorization scratch lives there);
+// mark(id): internal phase marks 60-64 (the caller records them after the sweep).
+template <int N, class Pre, class Mark>
+__device__ __forceinline__ void schur_gj_mfma(const double (&S)[64], SchurLds<N>& F, int t, Pre&& pre, Mark&& mark) {
+  constexpr int NI = SchurCfg<N>::NI, QS = SchurCfg<N>::QS, NB = (NI + 15) / 16;
+  const int j = t & 15, grp = t >> 4;
+  mf4 X[NB][NB];
+  // the upper tiles: X[I][J][v] in row g = S[16 I + 4 v + g] of lane 16 J + j, plus the identity
+#pragma unroll
+  for (int I = 0; I < NB; ++I)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      double y[4] = {S[16 * I + 4 * v], S[16 * I + 4 * v + 1], S[16 * I + 4 * v + 2], S[16 * I + 4 * v + 3]};
+      transpose_rows(y);
+#pragma unroll
+      for (int J = I; J < NB; ++J) X[I][J][v] = y[J] + ((I == J && j == 4 * v + grp) ? 1.0 : 0.0);
+    }
+  mark(60);  // tiles made
+  const mf4 zero = {0.0, 0.0, 0.0, 0.0};
+  // LDS staging above the live scratch (R'^-1): the pivot tile, then one buffer per transposed tile
+  double* stage = F.Q + 64 * N;
+  static_assert(64 * N + 256 * NB <= NI * QS + 2, "staging inside Q");
+  auto to_rows = [&](const mf4& d, double (&R)[16]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) stage[16 * (4 * v + grp) + j] = d[v];
+    wave_sync();
+    const double2* r2 = reinterpret_cast<const double2*>(stage + 16 * j);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const double2 w = r2[c];
+      R[2 * c] = w.x;
+      R[2 * c + 1] = w.y;
+    }
+    wave_sync();
+  };
+  auto from_rows = [&](const double (&R)[16]) __attribute__((always_inline)) {
+    mf4 d;
+    const bool b0 = (grp & 1) != 0, b1 = (grp & 2) != 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const double lo = b0 ? R[4 * v + 1] : R[4 * v], hi = b0 ? R[4 * v + 3] : R[4 * v + 2];
+      d[v] = b1 ? hi : lo;
+    }
+    return d;
+  };
+  constexpr int PV0 = NI < 16 ? NI : 16;
+  mf4 P;
+  {
+    double R[16];
+    to_rows(X[0][0], R);
+    gj_rows<PV0>(R, j, [](auto) {});
+    P = from_rows(R);
+  }
+  mark(61);  // first pivot tile swept
+  sfor<0, NB>([&](auto K) __attribute__((always_inline)) {
+    constexpr int k = decltype(K)::value;
+    constexpr int PV = NI - 16 * k < 16 ? NI - 16 * k : 16;
+    constexpr int KB = (PV + 3) / 4;
+    using Plan = GjPlanSym<NB, k>;
+    constexpr int kn = Plan::kn, n1 = Plan::count(1), n2 = Plan::count(2), NT = (n1 + n2) * KB;
+    // row k before the step: X_kj (j > k, kept as is) and X_kj = -X_jk' (j < k, transposed here)
+    mf4 T[NB];
+#pragma unroll
+    for (int jj = 0; jj < k; ++jj) {
+      double* buf = stage + 256 * (1 + jj);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) buf[16 * (4 * v + grp) + j] = X[jj][k][v];
+      wave_sync();
+#pragma unroll
+      for (int v = 0; v < 4; ++v) T[jj][v] = -buf[16 * j + 4 * v + grp];
+    }
+#pragma unroll
+    for (int jj = k + 1; jj < NB; ++jj) T[jj] = X[k][jj];
+    mf4 NA[NB];  // (-X_ak)' = -s X_ka for a != k
+#pragma unroll
+    for (int a = 0; a < NB; ++a)
+      if (a != k) NA[a] = a < k ? T[a] : -T[a];
+    mark(62);  // row k transposed
+    mf4 RP[NB];
+    auto issue = [&](auto TT) __attribute__((always_inline)) {
+      constexpr int tt = decltype(TT)::value;
+      constexpr bool g1 = tt < n1 * KB;
+      constexpr int kb = g1 ? tt / n1 : (tt - n1 * KB) / n2;
+      constexpr int cd = g1 ? Plan::list(1, tt % n1) : Plan::list(2, (tt - n1 * KB) % n2);
+      constexpr int kind = cd / 100, a = (cd / 10) % 10, b = cd % 10;
+#ifdef MPCQP_GJ_DBG_NOTASK  // (microbenchmark builds only: timing without the MFMA tasks)
+      if constexpr (true) {
+      } else
+#endif
+      if constexpr (kind == 0)
+        RP[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(P[kb], T[b][kb], kb == 0 ? zero : RP[b], 0, 0, 0);
+      else if constexpr (b == kn)
+        X[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(NA[a][kb], X[k][kn][kb], X[a][b], 0, 0, 0);
+      else
+        X[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(NA[a][kb], RP[b][kb], X[a][b], 0, 0, 0);
+    };
+    if constexpr (kn >= 0) {
+      // the next pivot tile's panel and update (a chain of 2 KB dependent MFMAs)
+      X[k][kn] = mfma_chain<0, KB>(P, T[kn], zero);
+      X[kn][kn] = mfma_chain<0, KB>(NA[kn], X[k][kn], X[kn][kn]);
+      constexpr int PVn = NI - 16 * kn < 16 ? NI - 16 * kn : 16;
+      double R[16];
+      to_rows(X[kn][kn], R);
+      mark(63);  // lookahead done, next pivot tile in rows
+#ifdef MPCQP_GJ_DBG_NOROWS  // (microbenchmark builds only: timing without the pivot sweeps)
+      sfor<0, NT>(issue);
+      if constexpr (false)
+#endif
+      gj_rows<PVn>(R, j, [&](auto Pp) __attribute__((always_inline)) {
+        constexpr int p = decltype(Pp)::value;
+        sfor<p * NT / PVn, (p + 1) * NT / PVn>(issue);
+      });
+#pragma unroll
+      for (int jj = 0; jj < NB; ++jj)
+        if (jj != k && jj != kn) X[k][jj] = RP[jj];
+      X[k][k] = P;
+      P = from_rows(R);
+    } else {
+      sfor<0, NT>(issue);
+#pragma unroll
+      for (int jj = 0; jj < NB; ++jj)
+        if (jj != k) X[k][jj] = RP[jj];
+      X[k][k] = P;
+    }
+    mark(64);  // step done
+  });
+  pre();
+  wave_sync();
+  // Q = I - X from the kept tiles (diagonal, and (b, a) with b > a: X_ab = X_ba', S^-1 symmetric);
+  // columns 16 NB .. QS-1 of a short horizon: zero
+  if constexpr (16 * NB < QS) {
+    if (t < NI)
+#pragma unroll
+      for (int m = 16 * NB; m < QS; m += 2) *reinterpret_cast<double2*>(&F.Q[QS * t + m]) = make_double2(0.0, 0.0);
+  }
+#pragma unroll
+  for (int I = 0; I < NB; ++I)
+#pragma unroll
+    for (int J = 0; J <= I; ++J)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int r = 16 * I + 4 * v + grp, c = 16 * J + j;
+        const double x = ((I == J && j == 4 * v + grp) ? 1.0 : 0.0) - X[I][J][v];
+        if (r < NI && c < QS) F.Q[QS * r + c] = x;
+        if (I != J && c < NI && r < QS) F.Q[QS * c + r] = x;
+      }
+  if (t == 0) *reinterpret_cast<double2*>(&F.Q[QS * NI]) = make_double2(0.0, 0.0);
+}
+#endif
+
 // alpha_jl of M (integer valued, exact in binary64): sum_{i=max(j,l)}^{N-1} (i - j)(i - l)
 __device__ __forceinline__ double alpha_jl(int N, int j, int l) {
   const int M = j > l ? j : l, K = N - 1, cnt = K - M + 1;
   const int s1 = (M + K) * cnt / 2;
   const int s2 = K * (K + 1) * (2 * K + 1) / 6 - (M - 1) * M * (2 * M - 1) / 6;
   return (double)(s2 - (j + l) * s1 + j * l * cnt);
+}
+
+// The in-register scalar sweep (MPCQP_GJ_MFMA == 0): S - I in the lane's row (lane t = row t) ->
+// Q = I - S^-1 in F.Q.  pre(): run after the sweep, before the first store to Q.
+template <int N, class Pre>
+__device__ __forceinline__ void schur_gj_valu(double (&S)[64], SchurLds<N>& F, int t, Pre&& pre) {
+  constexpr int NI = SchurCfg<N>::NI, QS = SchurCfg<N>::QS;
+  const int i = t < NI ? t : NI - 1;
+  const bool iv = t < NI;
+  // In-place Gauss-Jordan inverse of S (SPD: no pivoting).  With pivots 0..p-1 done, the current
+  // matrix X has X[p][j] = X[j][p] for j >= p and X[p][j] = -X[j][p] for j < p, so row p is lane
+  // j's own column p with a sign: each pivot makes four 16-lane row copies of it with the
+  // row-swap permutes and every lane applies X[t][j] += X[p][j] g_t with row_newbcast FMAs.
+  // Software-pipelined: the chunk holding the next pivot's column is updated first, then the next
+  // pivot's row broadcast and reciprocal (a long dependent chain) are issued among the other chunks'
+  // independent FMAs.  Pad columns (>= NI) are skipped: their row entries are all zero.
+  struct Piv {
+    double x[4], g, newc;
+  };
+  auto prelude = [&](auto P) __attribute__((always_inline)) {
+    constexpr int pv = decltype(P)::value;
+    Piv o;
+    const double col = S[pv] + (t == pv ? 1.0 : 0.0);
+    const double rj = t < pv ? -col : col;
+    // row p of the current matrix in every DPP row, absolute column order (copy s' = columns
+    // 16 s' .. 16 s' + 15); the pivot X[p][p] is lane p & 15 of copy p >> 4
+    rowbcast4(rj, o.x[0], o.x[1], o.x[2], o.x[3]);
+    asm("" : "+&v"(o.x[0]), "+&v"(o.x[1]), "+&v"(o.x[2]), "+&v"(o.x[3]));  // all four made here
+    const double a0 = __builtin_amdgcn_update_dpp(0.0, o.x[pv >> 4], 0x150 + (pv & 15), 0xF, 0xF, false);
+    const double pinv = recip(a0);
+    const double cp = col * pinv;
+    o.g = t == pv ? pinv - 1.0 : -cp;
+    o.newc = t == pv ? pinv : -cp;
+    return o;
+  };
+  Piv cur = prelude(IC<0>{});
+  sfor<0, NI>([&](auto P) __attribute__((always_inline)) {
+    constexpr int pv = decltype(P)::value;
+    constexpr int cs = (pv + 1 < NI ? pv + 1 : pv) >> 4;
+    upd_chunk<cs, NI>(cur.x[cs], cur.g, S);
+    Piv nxt;
+    if constexpr (pv + 1 < NI) nxt = prelude(IC<pv + 1>{});
+    // (the other chunks' row copies were made with the first one's, before its update: no wait)
+    if constexpr (cs != 0) upd_chunk<0, NI, false>(cur.x[0], cur.g, S);
+    if constexpr (cs != 1) upd_chunk<1, NI, false>(cur.x[1], cur.g, S);
+    if constexpr (cs != 2) upd_chunk<2, NI, false>(cur.x[2], cur.g, S);
+    if constexpr (cs != 3) upd_chunk<3, NI, false>(cur.x[3], cur.g, S);
+    S[pv] = cur.newc;
+    if constexpr (pv + 1 < NI) cur = nxt;
+  });
+  pre();
+  wave_sync();
+  // Q = I - S^-1 (columns NI .. QS-1: 0; the last row's tail: 0): -S^-1, then each row's diagonal
+  if (iv) {
+#pragma unroll
+    for (int m = 0; m < QS; m += 2) {
+      const double q0 = m < NI ? -S[m] : 0.0;
+      const double q1 = m + 1 < NI ? -S[m + 1] : 0.0;
+      *reinterpret_cast<double2*>(&F.Q[QS * i + m]) = make_double2(q0, q1);
+    }
+    F.Q[QS * i + i] += 1.0;
+  }
+  if (t == 0) *reinterpret_cast<double2*>(&F.Q[QS * NI]) = make_double2(0.0, 0.0);
+  wave_sync();
 }
 
 // ---- factorization (once per rho) ----------------------------------------------------------------
@@ -400,74 +783,55 @@ __device__ __forceinline__ void schur_factor(SM& sm, SchurLds<N>& F, const mpcqp
       }
     });
   });
-  // S holds L'CL so far: the identity is added to each diagonal entry when its pivot comes (entry
-  // (j, j) is read first by pivot j; the updates before it never read it) and pad rows stay 0.
-  // In-place Gauss-Jordan inverse of S (SPD: no pivoting).  With pivots 0..p-1 done, the current
-  // matrix X has X[p][j] = X[j][p] for j >= p and X[p][j] = -X[j][p] for j < p, so row p is lane
-  // j's own column p with a sign: each pivot makes four 16-lane row copies of it with the
-  // row-swap permutes and every lane applies X[t][j] += X[p][j] g_t with row_newbcast FMAs.
+  // S holds L'CL so far: the sweep adds the identity (schur_gj_valu: to each diagonal entry when its
+  // pivot comes, entry (j, j) being read first by pivot j; the MFMA forms: to the tiles) and pad rows
+  // stay 0.
   mark(14);
-  // Software-pipelined: the chunk holding the next pivot's column is updated first, then the next
-  // pivot's row broadcast and reciprocal (a long dependent chain) are issued among the other chunks'
-  // independent FMAs.  Pad columns (>= NI) are skipped: their row entries are all zero.
-  struct Piv {
-    double x[4], g, newc;
+#if MPCQP_GJ_MFMA
+  // internal marks: cycle counts kept in registers, recorded after the sweep (no branch inside it)
+  long long gts[12];
+  int gid[12], ng = 0;
+  auto stamp = [&](int id) __attribute__((always_inline)) {
+#ifdef MPCQP_PHASE_TIMING
+    gid[ng] = id;
+    gts[ng] = (long long)__builtin_readcyclecounter();
+    ++ng;
+#endif
+    (void)id;
   };
-  auto prelude = [&](auto P) __attribute__((always_inline)) {
-    constexpr int pv = decltype(P)::value;
-    Piv o;
-    const double col = S[pv] + (t == pv ? 1.0 : 0.0);
-    const double rj = t < pv ? -col : col;
-    // row p of the current matrix in every DPP row, absolute column order (copy s' = columns
-    // 16 s' .. 16 s' + 15); the pivot X[p][p] is lane p & 15 of copy p >> 4
-    rowbcast4(rj, o.x[0], o.x[1], o.x[2], o.x[3]);
-    asm("" : "+&v"(o.x[0]), "+&v"(o.x[1]), "+&v"(o.x[2]), "+&v"(o.x[3]));  // all four made here
-    const double a0 = __builtin_amdgcn_update_dpp(0.0, o.x[pv >> 4], 0x150 + (pv & 15), 0xF, 0xF, false);
-    const double pinv = recip(a0);
-    const double cp = col * pinv;
-    o.g = t == pv ? pinv - 1.0 : -cp;
-    o.newc = t == pv ? pinv : -cp;
-    return o;
-  };
-  Piv cur = prelude(IC<0>{});
-  sfor<0, NI>([&](auto P) __attribute__((always_inline)) {
-    constexpr int pv = decltype(P)::value;
-    constexpr int cs = (pv + 1 < NI ? pv + 1 : pv) >> 4;
-    upd_chunk<cs, NI>(cur.x[cs], cur.g, S);
-    Piv nxt;
-    if constexpr (pv + 1 < NI) nxt = prelude(IC<pv + 1>{});
-    // (the other chunks' row copies were made with the first one's, before its update: no wait)
-    if constexpr (cs != 0) upd_chunk<0, NI, false>(cur.x[0], cur.g, S);
-    if constexpr (cs != 1) upd_chunk<1, NI, false>(cur.x[1], cur.g, S);
-    if constexpr (cs != 2) upd_chunk<2, NI, false>(cur.x[2], cur.g, S);
-    if constexpr (cs != 3) upd_chunk<3, NI, false>(cur.x[3], cur.g, S);
-    S[pv] = cur.newc;
-    if constexpr (pv + 1 < NI) cur = nxt;
-  });
-  mark(15);
-  // the lane's rows of R'^-1, read back from the scratch (before Q overwrites it)
+  schur_gj_mfma<N>(
+      S, F, t,
+      [&]() __attribute__((always_inline)) {
+        // the lane's rows of R'^-1, read back from the scratch (before Q overwrites it)
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int kk = 4 * r + ig;
-    const int kc = kk < N ? kk : N - 1;
-    const double* ri = sc.Ri[kc][leg] + 3 * (av ? a : 2);
-    RI[r][0] = ri[0];
-    RI[r][1] = ri[1];
-    RI[r][2] = ri[2];
-  }
+        for (int r = 0; r < R; ++r) {
+          const int kk = 4 * r + ig;
+          const int kc = kk < N ? kk : N - 1;
+          const double* ri = sc.Ri[kc][leg] + 3 * (av ? a : 2);
+          RI[r][0] = ri[0];
+          RI[r][1] = ri[1];
+          RI[r][2] = ri[2];
+        }
+      },
+      stamp);
   wave_sync();
-  // Q = I - S^-1 (columns NI .. QS-1: 0; the last row's tail: 0): -S^-1, then each row's diagonal
-  if (iv) {
+  mark(15);  // (after the stores to Q: f_gj covers them)
+  for (int e = 0; e < ng; ++e) mark(gid[e], gts[e]);
+#else
+  schur_gj_valu<N>(S, F, t, [&]() __attribute__((always_inline)) {
+    mark(15);
+    // the lane's rows of R'^-1, read back from the scratch (before Q overwrites it)
 #pragma unroll
-    for (int m = 0; m < QS; m += 2) {
-      const double q0 = m < NI ? -S[m] : 0.0;
-      const double q1 = m + 1 < NI ? -S[m + 1] : 0.0;
-      *reinterpret_cast<double2*>(&F.Q[QS * i + m]) = make_double2(q0, q1);
+    for (int r = 0; r < R; ++r) {
+      const int kk = 4 * r + ig;
+      const int kc = kk < N ? kk : N - 1;
+      const double* ri = sc.Ri[kc][leg] + 3 * (av ? a : 2);
+      RI[r][0] = ri[0];
+      RI[r][1] = ri[1];
+      RI[r][2] = ri[2];
     }
-    F.Q[QS * i + i] += 1.0;
-  }
-  if (t == 0) *reinterpret_cast<double2*>(&F.Q[QS * NI]) = make_double2(0.0, 0.0);
-  wave_sync();
+  });
+#endif
 }
 
 // ---- KKT solve (every ADMM iteration) ------------------------------------------------------------

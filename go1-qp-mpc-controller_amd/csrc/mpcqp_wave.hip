@@ -1143,12 +1143,14 @@ __device__ __forceinline__ FusedScale scale_wave(WSmem<N, 1>& sm, const mpcqp_pa
 #define WV_MARK_ON(id) true
 #define WV_HWID() 0.0
 #endif
-#define WV_MARK(id)                                                                     \
+#define WV_MARK(id) WV_MARK_AT(id, -1)
+// cyc >= 0: a cycle count taken earlier (marks recorded in registers inside straight-line code)
+#define WV_MARK_AT(id, cyc)                                                             \
   do {                                                                                  \
     if (WV_MARK_ON(id) && trace && threadIdx.x == 0 && inst < trace_cap && nmark < MPCQP_TRACE_LEN) { \
       double* tm_ = trace + ((size_t)inst * MPCQP_TRACE_LEN + nmark) * 4;                \
       tm_[0] = (id);                                                                    \
-      tm_[1] = (double)__builtin_readcyclecounter();                                    \
+      tm_[1] = (cyc) >= 0 ? (double)(cyc) : (double)__builtin_readcyclecounter();       \
       tm_[2] = (double)__builtin_amdgcn_s_memrealtime();                                \
       tm_[3] = WV_HWID();                                                               \
       ++nmark;                                                                          \
@@ -1160,6 +1162,9 @@ __device__ __forceinline__ FusedScale scale_wave(WSmem<N, 1>& sm, const mpcqp_pa
 #else
 #define WV_MARK(id) \
   do {              \
+  } while (0)
+#define WV_MARK_AT(id, cyc) \
+  do {                      \
   } while (0)
 #endif
 
@@ -1602,7 +1607,12 @@ __device__ __forceinline__ bool wave_solve(const int inst, WSmem<N, KS>& sm, con
       else {
         double smax;
         schur_factor<N, R>(sm, F, p, A, cost_c, dtm, SRI,
-                           [&](int id) __attribute__((always_inline)) { WV_MARK(id); (void)id; }, smax);
+                           [&](int id, long long cyc = -1) __attribute__((always_inline)) {
+                             WV_MARK_AT(id, cyc);
+                             (void)id;
+                             (void)cyc;
+                           },
+                           smax);
         // The push-through identity subtracts B'(I - S^-1)B w from R'^-1 w: with S ill-conditioned
         // (large state weights, four feet in contact) the difference loses digits the Riccati form
         // keeps.  Such a robot leaves the loop at the next need_info iteration (one follows every
