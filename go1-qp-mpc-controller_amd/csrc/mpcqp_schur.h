@@ -27,10 +27,13 @@
 #pragma once
 #include "mpcqp_wave_common.h"
 
-// 1: Q = I - S^-1 by the blocked Gauss-Jordan sweep on the matrix cores (schur_gj_mfma); 0: the
-// in-register scalar sweep (schur_gj_valu)
+// 1 (default): Q = I - S^-1 by the blocked Gauss-Jordan sweep on the matrix cores (schur_gj_mfma);
+// 0: the in-register scalar sweep (schur_gj_valu).  Same box, 3 repetitions
+// (profiles/r06/gj_mfma/ab_final.txt): C2 1.549 -> 1.537 ms, C5 2.925 -> 2.901 ms; the sweep alone
+// 30.6k -> 27.1k cycles (tools/mb/mb_gjsweep).  Built with -mllvm -amdgpu-mfma-vgpr-form (Makefile):
+// MFMA results in VGPRs, without which the tiles spill.
 #ifndef MPCQP_GJ_MFMA
-#define MPCQP_GJ_MFMA 0
+#define MPCQP_GJ_MFMA 1
 #endif
 
 namespace mpcqp {

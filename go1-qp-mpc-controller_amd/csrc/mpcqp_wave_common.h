@@ -136,6 +136,12 @@ struct WSmem {
 // One accumulator per mat-vec, the terms in column order: a dependent v_fmac_f64_dpp chain issues as
 // fast as independent ones for a lone wave (4.4 against 5.35 cycles, tools/mb/mb_valu), so rotating
 // accumulators only cost the zeroing moves and the closing adds (the round-4 form: MPCQP_MV_MULTI_ACC).
+// Each FMA reads the accumulator its predecessor just wrote.  The DPP wait-state requirement (VALU
+// write, then a DPP read of that VGPR: 2 states) concerns the operand read through the lane permute,
+// src0 (here x, written before the block's head wait); the accumulator is an ordinary dependent VALU
+// operand.  LLVM's hazard recognizer applies the rule to every operand of a DPP instruction, so this
+// reading is not the compiler's: tools/mb/mb_valu checks the chain numerically on MI355X (bitwise the
+// host's fma chain) beside the src0 case it does not cover.
 #define WV_OPS12(P, C) [P##0] "v"(C[0]), [P##1] "v"(C[1]), [P##2] "v"(C[2]), [P##3] "v"(C[3]), [P##4] "v"(C[4]), \
     [P##5] "v"(C[5]), [P##6] "v"(C[6]), [P##7] "v"(C[7]), [P##8] "v"(C[8]), [P##9] "v"(C[9]),                \
     [P##10] "v"(C[10]), [P##11] "v"(C[11])

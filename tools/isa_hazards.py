@@ -228,7 +228,8 @@ def main():
     if path is None:
         path = os.path.join(tempfile.mkdtemp(), "w.s")
         nflag = [] if a.all else [f"-DMPCQP_WAVE_FOR_EACH_N(X)=X({a.n})"]
-        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-strict-aliasing"]
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-strict-aliasing",
+                        "-mllvm", "-amdgpu-mfma-vgpr-form"]
                        + nflag + ["--cuda-device-only", "-S", SRC, "-o", path] + a.defs
                        + os.environ.get("ISA_EXTRA_FLAGS", "").split(),
                        check=True, stderr=subprocess.DEVNULL)

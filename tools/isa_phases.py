@@ -16,6 +16,7 @@ SRC = os.path.join(REPO, "go1-qp-mpc-controller_amd", "csrc", "mpcqp_wave.hip")
 
 def compile_asm(n, defs, out, src=SRC):
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fno-strict-aliasing",
+           "-mllvm", "-amdgpu-mfma-vgpr-form",
            "-DMPCQP_ISA_MARKS", f"-DMPCQP_WAVE_FOR_EACH_N(X)=X({n})", "--cuda-device-only", "-S", src,
            "-o", out] + defs
     subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)

@@ -2,12 +2,18 @@
 // SIMD (the solver's occupancy): independent v_fmac_f64 (plain and DPP row_newbcast), dependent
 // chains of each, v_permlane16/32_swap, v_mov_b64_dpp, s_nop, v_accvgpr moves.  Cycles per
 // instruction from s_memtime around 64 x 16-instruction blocks, median over the workgroups.
+// Numeric check (exit status 1 on a mismatch): the single-accumulator mat-vec chain of
+// mpcqp_wave_common.h (mv12: twelve v_fmac_f64_dpp row_newbcast into one accumulator, each reading
+// the accumulator its predecessor wrote with no wait state between them) against the host's fma
+// chain, bitwise; and, for reference, the hazard the wait states guard: the DPP source written by the
+// instruction just before.
 //   hipcc -O3 --offload-arch=gfx950 tools/mb/mb_valu.hip -o tools/mb/mb_valu && tools/mb/mb_valu
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #define REP16(X) X X X X X X X X X X X X X X X X
@@ -90,6 +96,51 @@ KERNEL(k_d4c, B_D4C, 128)
   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(g));
 KERNEL(k_p4c, B_P4C, 128)
 
+// the mv12 chain: a += bcast_L(x) * c[n] over the twelve lanes L of WV_M12, one accumulator
+#define CK(N, L) "v_fmac_f64_dpp %[a], %[x], %[c" #N "] row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#define CK12 CK(0, 0) CK(1, 1) CK(2, 2) CK(3, 4) CK(4, 5) CK(5, 6) CK(6, 8) CK(7, 9) CK(8, 10) CK(9, 12) CK(10, 13) CK(11, 14)
+#define CK_OPS [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]), \
+    [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]), [c9] "v"(c[9]), [c10] "v"(c[10]), [c11] "v"(c[11])
+__global__ __launch_bounds__(64) void k_check(const double* xin, const double* cin, double* out, int hazard) {
+  const int t = threadIdx.x;
+  double x = xin[t], c[12];
+  for (int n = 0; n < 12; ++n) c[n] = cin[12 * t + n];
+  double a = 0.0;
+  if (hazard)  // x rewritten by the instruction just before the first DPP read of it
+    asm volatile("s_nop 4\n\tv_add_f64 %[x], %[x], 1.0\n\t" CK12 : [a] "+v"(a), [x] "+v"(x) : CK_OPS);
+  else
+    asm volatile("s_nop 4\n\t" CK12 : [a] "+v"(a) : [x] "v"(x), CK_OPS);
+  out[t] = a;
+}
+static int check_chain(bool hazard) {
+  double hx[64], hc[64 * 12], ho[64], *dx, *dc, *dout;
+  for (int t = 0; t < 64; ++t) {
+    hx[t] = 1.0 / (3.0 + t) - 0.125 * (t & 7);
+    for (int n = 0; n < 12; ++n) hc[12 * t + n] = 0.37 * n - 1.0 / (1.0 + t + n);
+  }
+  hipMalloc(&dx, sizeof(hx));
+  hipMalloc(&dc, sizeof(hc));
+  hipMalloc(&dout, sizeof(ho));
+  hipMemcpy(dx, hx, sizeof(hx), hipMemcpyHostToDevice);
+  hipMemcpy(dc, hc, sizeof(hc), hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_check, dim3(1), dim3(64), 0, 0, dx, dc, dout, hazard ? 1 : 0);
+  hipMemcpy(ho, dout, sizeof(ho), hipMemcpyDeviceToHost);
+  const int lanes[12] = {0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14};
+  int bad = 0;
+  for (int t = 0; t < 64; ++t) {
+    double a = 0.0;
+    for (int n = 0; n < 12; ++n) {
+      const double xb = hx[16 * (t / 16) + lanes[n]] + (hazard ? 1.0 : 0.0);
+      a = std::fma(xb, hc[12 * t + n], a);
+    }
+    bad += a != ho[t];
+  }
+  hipFree(dx);
+  hipFree(dc);
+  hipFree(dout);
+  return bad;
+}
+
 typedef void (*kfn)(double*, long long*, int);
 int main() {
   const int blocks = 1024, iters = 200;  // one 64-thread wave per SIMD on 256 CUs
@@ -118,5 +169,8 @@ int main() {
     const double med = (double)cyc[blocks / 2] / ((double)iters * k.ins);
     printf("%-28s %6.2f cycles/instruction (median over %d waves)\n", k.name, med, blocks);
   }
-  return 0;
+  const int bad = check_chain(false), bad_h = check_chain(true);
+  printf("dependent DPP FMA chain, one accumulator (mv12 form): %d of 64 lanes differ from the host fma chain\n", bad);
+  printf("(reference) DPP source written 0 wait states before: %d of 64 lanes differ\n", bad_h);
+  return bad ? 1 : 0;
 }
