@@ -31,3 +31,12 @@ def test_product_kernels_have_no_isa_hazards():
     for n, o in zip(horizons, outs):
         assert o.returncode == 0, f"N={n}:\n{o.stdout[-3000:]}{o.stderr[-2000:]}"
         assert o.stdout.count("hazards none") == len(_kernels(n)), f"N={n}:\n{o.stdout}"
+
+
+def test_scalar_sweep_build_has_no_isa_hazards():
+    """The in-register scalar Gauss-Jordan (-DMPCQP_GJ_MFMA=0, the pre-round-6 default kept as a
+    build option) still compiles hazard-free at N = 10."""
+    cmd = [sys.executable, os.path.join(REPO, "tools", "isa_hazards.py"), "--n", "10", "--defs=-DMPCQP_GJ_MFMA=0",
+           "--kernels", "wave_kernelILi10ELi1E"]
+    o = subprocess.run(cmd, capture_output=True, text=True, timeout=1200)
+    assert o.returncode == 0 and "hazards none" in o.stdout, o.stdout[-3000:] + o.stderr[-2000:]
