@@ -115,6 +115,17 @@ def test_other_horizons_p1(oracle, N):
         _check_p1(oracle, s, recs, f"N={N}")
 
 
+@pytest.mark.parametrize("N", [2, 3, 5, 6, 8, 9, 10])
+def test_every_schur_horizon_mixed_p1(oracle, N):
+    """Every Schur-form horizon, mixed gait (more rho updates, so more factorizations): the
+    matrix-core Gauss-Jordan runs with 1 (N <= 2), 2 (3..5), 3 (6..8) and 4 (9, 10) block rows, the
+    last short (6N mod 16 real rows) except at N = 8."""
+    st = mpcqp.synthetic_go1(32, seed=300 + N, gait="mixed", mixed_mu=True)
+    recs = mpcqp.assemble_compute_grf(st, N)
+    with mpcqp.MpcQpSolver(mpcqp.default_params(N)) as s:
+        _check_p1(oracle, s, recs, f"N={N} mixed")
+
+
 def test_converged_p2(oracle):
     """Converged mode: both sides run to eps 1e-9; robust to rho-schedule details."""
     p = mpcqp.default_params(10, eps_abs=1e-9, eps_rel=1e-9, max_iter=20000)
