@@ -366,7 +366,9 @@ __device__ __forceinline__ void schur_gj_mfma(const double (&S)[64], SchurLds<N>
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       double y[4] = {S[16 * I + 4 * v], S[16 * I + 4 * v + 1], S[16 * I + 4 * v + 2], S[16 * I + 4 * v + 3]};
+#ifndef MPCQP_GJ_DBG_NOCONV  // (microbenchmark builds only: timing without the tile transposes)
       transpose_rows(y);
+#endif
 #pragma unroll
       for (int J = I; J < NB; ++J) X[I][J][v] = y[J] + ((I == J && j == 4 * v + grp) ? 1.0 : 0.0);
     }
@@ -481,6 +483,7 @@ __device__ __forceinline__ void schur_gj_mfma(const double (&S)[64], SchurLds<N>
   });
   pre();
   wave_sync();
+#ifndef MPCQP_GJ_DBG_NOSTORE  // (microbenchmark builds only: timing without the stores to Q)
   // Q = I - X from the kept tiles (diagonal, and (b, a) with b > a: X_ab = X_ba', S^-1 symmetric);
   // columns 16 NB .. QS-1 of a short horizon: zero
   if constexpr (16 * NB < QS) {
@@ -488,6 +491,13 @@ __device__ __forceinline__ void schur_gj_mfma(const double (&S)[64], SchurLds<N>
 #pragma unroll
       for (int m = 16 * NB; m < QS; m += 2) *reinterpret_cast<double2*>(&F.Q[QS * t + m]) = make_double2(0.0, 0.0);
   }
+#ifdef MPCQP_GJ_STORE_SEL
+  // branch-free stores: an entry outside Q (pad rows / columns) goes to the lane's own slot of qv,
+  // which the KKT solve and P~x write before they read it.  0.9k cycles less per factorization in
+  // tools/mb/mb_gjsweep, but C2 / C5 unchanged within noise in the product (profiles/r06/gj_mfma/
+  // store_ab.txt): off
+  double* const dummy = &F.qv[t];
+#endif
 #pragma unroll
   for (int I = 0; I < NB; ++I)
 #pragma unroll
@@ -496,9 +506,26 @@ __device__ __forceinline__ void schur_gj_mfma(const double (&S)[64], SchurLds<N>
       for (int v = 0; v < 4; ++v) {
         const int r = 16 * I + 4 * v + grp, c = 16 * J + j;
         const double x = ((I == J && j == 4 * v + grp) ? 1.0 : 0.0) - X[I][J][v];
+#ifdef MPCQP_GJ_STORE_SEL
+        *(r < NI && c < QS ? &F.Q[QS * r + c] : dummy) = x;
+        if (I != J) *(c < NI && r < QS ? &F.Q[QS * c + r] : dummy) = x;
+#else
         if (r < NI && c < QS) F.Q[QS * r + c] = x;
         if (I != J && c < NI && r < QS) F.Q[QS * c + r] = x;
+#endif
       }
+#else
+  {  // keep the sweep's results live
+    double ck = 0.0;
+#pragma unroll
+    for (int I = 0; I < NB; ++I)
+#pragma unroll
+      for (int J = 0; J <= I; ++J)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) ck += X[I][J][v];
+    F.qv[t] = ck;
+  }
+#endif
   if (t == 0) *reinterpret_cast<double2*>(&F.Q[QS * NI]) = make_double2(0.0, 0.0);
 }
 #endif
