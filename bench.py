@@ -381,9 +381,9 @@ def run_rank(args):
                                    "handle's internal streams; a rocprofv3 kernel trace gives the same span as "
                                    "the first launch's start to the last launch's end of each step "
                                    "(tools/trace_span.py)"),
-                "note": ("binary64 on the VALU (v_fmac_f64 DPP): "
+                "note": ("binary64 on the VALU (v_fmac_f64 DPP) and the matrix cores (v_mfma_f64_16x16x4f64): "
                          + ("impulse-space Schur-form KKT solve (one dense 6N x 6N mat-vec per ADMM "
-                            "iteration, in-register Gauss-Jordan per rho)" if N <= 10 else
+                            "iteration, blocked Gauss-Jordan per rho on the matrix cores)" if N <= 10 else
                             "Riccati-form KKT solve (chains of 12x12 mat-vecs per iteration, factorization "
                             "on v_mfma_f64_16x16x4f64)")
                          + "; FLOPs = SURVEY §8(d)'s structure-exploiting count per robot with its actual "

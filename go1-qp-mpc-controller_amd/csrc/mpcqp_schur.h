@@ -17,7 +17,7 @@
 // eigenvalues >= 1, condition ~1e0-1e3 on the Go1 workload):
 //   (c B6'M B6 + R')^-1 w = R'^-1 w - B' (I - S^-1) B w,   B := Li B6 R'^-1  (6N x 12N, per step 6x12)
 // (push-through identity; exact in real arithmetic).  Per factorization (rho change): R'^-1 per
-// foot, B (per step), S (6N x 6N) and Q = I - S^-1 by an in-register Gauss-Jordan sweep.  Per ADMM
+// foot, B (per step), S (6N x 6N) and Q = I - S^-1 by a blocked Gauss-Jordan sweep (schur_gj_mfma).  Per ADMM
 // iteration:  z = B w (6x12 per step),  q = Q z (dense, one lane per row of Q),  u = R'^-1 w - B' q.
 //
 // Lane roles inside the one wave of a robot: the ADMM layout of wave_kernel (variable lanes: step
