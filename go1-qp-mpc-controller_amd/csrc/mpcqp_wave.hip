@@ -1159,6 +1159,12 @@ __device__ __forceinline__ FusedScale scale_wave(WSmem<N, 1>& sm, const mpcqp_pa
 #elif defined(MPCQP_ISA_MARKS)
 // static ISA accounting (tools/isa_phases.py): an assembly comment per phase mark
 #define WV_MARK(id) asm volatile(";WV_MARK %0" ::"n"(id))
+// (the Gauss-Jordan's internal marks are recorded after the fact only in timing builds: never here)
+#define WV_MARK_AT(id, cyc) \
+  do {                      \
+    (void)(cyc);            \
+    WV_MARK(id);            \
+  } while (0)
 #else
 #define WV_MARK(id) \
   do {              \
